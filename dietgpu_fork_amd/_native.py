@@ -1,0 +1,144 @@
+"""ctypes binding of libdietgpu_amd.so (the C ABI in include/dietgpu_c.h).
+
+The HIP library is the only compute path: if it is missing this module raises
+at import time -- there is no CPU fallback.
+"""
+import ctypes
+import os
+import subprocess
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "_lib", "libdietgpu_amd.so")
+CSRC = os.path.join(_HERE, "csrc")
+
+DIETGPU_OK = 0
+DIETGPU_ERR_INVALID = 1
+DIETGPU_ERR_HIP = 2
+DIETGPU_ERR_CHECKSUM = 3
+
+
+class DietGpuError(RuntimeError):
+    pass
+
+
+class ChecksumMismatch(DietGpuError):
+    pass
+
+
+def build(jobs=8):
+    """Compile the HIP library for gfx950 in-tree (hipcc; no GPU needed)."""
+    subprocess.check_call(["make", "-s", f"-j{jobs}", "-C", CSRC])
+
+
+def _declare(L):
+    c_u32, c_u64, c_int, c_size, vp = (ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int,
+                                       ctypes.c_size_t, ctypes.c_void_p)
+    P = ctypes.c_void_p  # all device / host pointers passed as void*
+    sig = {
+        "dietgpu_last_error": (ctypes.c_char_p, []),
+        "dietgpu_version": (ctypes.c_char_p, []),
+        "dietgpu_stack_create": (vp, [c_int, P, c_size]),
+        "dietgpu_stack_destroy": (None, [vp]),
+        "dietgpu_stack_max_usage": (c_size, [vp]),
+        "dietgpu_stack_reset_max_usage": (None, [vp]),
+        "dietgpu_stack_size_total": (c_size, [vp]),
+        "dietgpu_get_max_compressed_size": (c_u32, [c_u32]),
+        "dietgpu_get_max_float_compressed_size": (c_u32, [c_int, c_u32]),
+        "dietgpu_get_max_sparse_float_compressed_size": (c_u32, [c_int, c_u32]),
+        "dietgpu_ans_encode_batch_stride": (c_int, [vp, c_int, c_int, c_u32, P, c_u32, c_u32, P,
+                                                    P, c_u32, P, P]),
+        "dietgpu_ans_encode_batch_pointer": (c_int, [vp, c_int, c_int, c_u32, P, P, P, P, P, P]),
+        "dietgpu_ans_encode_batch_split_size": (c_int, [vp, c_int, c_int, c_u32, P, P, P, P,
+                                                        c_u32, P, P]),
+        "dietgpu_ans_decode_batch_stride": (c_int, [vp, c_int, c_int, c_u32, P, c_u32, P, c_u32,
+                                                    c_u32, P, P, P]),
+        "dietgpu_ans_decode_batch_pointer": (c_int, [vp, c_int, c_int, c_u32, P, P, P, P, P, P]),
+        "dietgpu_ans_decode_batch_split_size": (c_int, [vp, c_int, c_int, c_u32, P, P, P, P, P,
+                                                        P]),
+        "dietgpu_ans_get_compressed_info": (c_int, [vp, P, c_u32, P, P, P]),
+        "dietgpu_ans_get_compressed_info_device": (c_int, [vp, P, c_u32, P, P, P]),
+        "dietgpu_float_compress": (c_int, [vp, c_int, c_int, c_int, c_u32, P, P, P, P, P]),
+        "dietgpu_float_compress_split_size": (c_int, [vp, c_int, c_int, c_int, c_u32, P, P, P,
+                                                      c_u32, P, P]),
+        "dietgpu_float_compress_sparse": (c_int, [vp, c_int, c_int, c_int, c_u32, P, P, P, P, P]),
+        "dietgpu_float_decompress": (c_int, [vp, c_int, c_int, c_int, c_u32, P, P, P, P, P, P]),
+        "dietgpu_float_decompress_split_size": (c_int, [vp, c_int, c_int, c_int, c_u32, P, P, P,
+                                                        P, P, P]),
+        "dietgpu_float_decompress_sparse": (c_int, [vp, c_int, c_int, c_int, c_u32, P, P, P, P,
+                                                    P, P]),
+        "dietgpu_float_get_compressed_info": (c_int, [vp, P, c_u32, P, P, P, P]),
+        "dietgpu_float_get_compressed_info_device": (c_int, [vp, P, c_u32, P, P, P, P]),
+        "dietgpu_float_compress_batch_stride": (c_int, [vp, c_int, c_int, c_int, c_u32, P, c_u32,
+                                                        c_u64, P, c_u64, P, P]),
+        "dietgpu_float_decompress_batch_stride": (c_int, [vp, c_int, c_int, c_int, c_u32, P,
+                                                          c_u64, P, c_u64, c_u32, P, P, P]),
+        "dietgpu_profile_enable": (None, [c_int]),
+        "dietgpu_profile_reset": (None, []),
+        "dietgpu_profile_query": (c_int, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_double),
+                                          ctypes.POINTER(ctypes.c_uint64)]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    return sig
+
+
+EXPORTED = None
+_lib = None
+
+
+def lib():
+    global _lib, EXPORTED
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(
+                f"dietgpu_fork_amd: HIP library not built ({LIB_PATH}); run "
+                "`python -c 'import __graft_entry__ as g; g.build()'`")
+        # torch first, so the process shares torch's HIP runtime (same soname)
+        import torch  # noqa: F401
+        L = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+        EXPORTED = sorted(_declare(L))
+        _lib = L
+    return _lib
+
+
+def check(rc):
+    if rc == DIETGPU_OK:
+        return
+    msg = lib().dietgpu_last_error().decode(errors="replace")
+    if rc == DIETGPU_ERR_CHECKSUM:
+        raise ChecksumMismatch(msg)
+    raise DietGpuError(msg)
+
+
+def ptr_array(values):
+    """Host array of pointers / uint32 for the C ABI (kept alive by caller)."""
+    return (ctypes.c_void_p * len(values))(*values)
+
+
+def u32_array(values):
+    return (ctypes.c_uint32 * len(values))(*values)
+
+
+class Stack:
+    """RAII wrapper of dietgpu_stack (StackDeviceMemory)."""
+
+    def __init__(self, device, ptr=None, nbytes=0):
+        self.h = lib().dietgpu_stack_create(int(device), ptr, int(nbytes))
+        if not self.h:
+            raise DietGpuError(lib().dietgpu_last_error().decode())
+
+    def max_usage(self):
+        return lib().dietgpu_stack_max_usage(self.h)
+
+    def close(self):
+        if self.h:
+            lib().dietgpu_stack_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,589 @@
+// Host orchestration of the MI355X rANS byte codec and float codec.
+// Implements the C++ API of include/dietgpu/GpuANSCodec.h and
+// include/dietgpu/GpuFloatCodec.h (reference: ans/GpuANSEncode.cu,
+// ans/GpuANSDecode.cu, ans/GpuANSInfo.cu, float/GpuFloatCompress.cu,
+// float/GpuFloatDecompress.cu, float/GpuFloatInfo.cu).
+//
+// Launch sequence per call (all stream-ordered, no host sync unless a
+// checksum has to be verified):
+//   compress:   k_hist -> k_normalize -> k_encode -> k_coalesce
+//   decompress: k_decode (table build + rANS decode + float join fused)
+#include <algorithm>
+#include <cstring>
+#include <sstream>
+#include <vector>
+
+#include "codec_internal.h"
+#include "dietgpu/GpuANSCodec.h"
+#include "dietgpu/GpuFloatCodec.h"
+#include "kernels.h"
+#include "profile.h"
+
+namespace dietgpu {
+
+namespace {
+constexpr uint32_t kMaxGridY = 65535;
+
+uint32_t histChunkWords(uint32_t nb, uint32_t maxSize) {
+  uint32_t chunk = 64 * 1024;
+  while (chunk > 4096 && uint64_t(nb) * divUp(std::max(maxSize, 1u), chunk) < 2048) chunk /= 2;
+  while (divUp(maxSize, chunk) > 4096) chunk *= 2;
+  return chunk;
+}
+
+void checkProbBits(int pb) {
+  DG_CHECK(pb >= 9 && pb <= 11, "unhandled pdf precision " << pb << " (must be 9, 10 or 11)");
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// generic drivers
+// ---------------------------------------------------------------------------
+template <int FT>
+void encodeBatchDevice(StackDeviceMemory& res, int pb, bool useChecksum, uint32_t nb,
+                       const BatchDesc& in, uint32_t maxSize, const uint32_t* hist_dev,
+                       const BatchDesc& out, uint32_t* outSize_dev, hipStream_t s) {
+  checkProbBits(pb);
+  if (nb == 0) return;
+  constexpr int kSegs = FloatTraits<FT>::kSegs;
+  const uint32_t MB = divUp(maxSize, kBlockSize);
+  const uint32_t chunkWords = histChunkWords(nb, maxSize);
+  const uint32_t chunks = std::max(1u, divUp(maxSize, chunkWords));
+  const bool userHist = FT == 0 && hist_dev != nullptr;
+  const bool runHist = !userHist || useChecksum;
+  const bool rawCk = FT == 0 && useChecksum;
+
+  auto partHist = res.alloc<uint32_t>(s, runHist ? size_t(kSegs) * nb * chunks * kNumSymbols : 1);
+  auto partCk = res.alloc<uint32_t>(s, rawCk ? size_t(nb) * chunks : 1);
+  auto ck = res.alloc<uint32_t>(s, nb);
+  auto table = res.alloc<uint4>(s, size_t(kSegs) * nb * kNumSymbols);
+  auto pdf = res.alloc<uint16_t>(s, size_t(kSegs) * nb * kNumSymbols);
+  auto slots = res.alloc<uint8_t>(s, size_t(kSegs) * nb * std::max(MB, 1u) * kSlotBytes);
+  auto cw = res.alloc<uint32_t>(s, size_t(kSegs) * nb * std::max(MB, 1u));
+
+  if (FT != 0 && useChecksum) {
+    HIP_CHECK(hipMemsetAsync(ck.data(), 0, sizeof(uint32_t) * nb, s));
+  }
+  for (uint32_t y0 = 0; y0 < nb; y0 += kMaxGridY) {
+    const uint32_t ny = std::min(kMaxGridY, nb - y0);
+    if (runHist) {
+      prof::Scope p("hist", s);
+      dim3 g(chunks, ny);
+      if (rawCk) {
+        k_hist<FT, true><<<g, kThreads, 0, s>>>(in, y0, nb, chunkWords, chunks, partHist.data(),
+                                                partCk.data());
+      } else {
+        k_hist<FT, false><<<g, kThreads, 0, s>>>(in, y0, nb, chunkWords, chunks, partHist.data(),
+                                                 nullptr);
+      }
+      HIP_LAUNCH_CHECK();
+    }
+    if (FT != 0 && useChecksum) {
+      // float checksum: the reference passes float-word counts as byte counts
+      // (float/GpuFloatCompress.cuh:709)
+      const uint32_t ckChunk = 1u << 20;
+      dim3 g(std::max(1u, divUp(maxSize, ckChunk)), ny);
+      k_checksum<<<g, kThreads, 0, s>>>(in, y0, 1, ckChunk, ck.data());
+      HIP_LAUNCH_CHECK();
+    }
+    {
+      prof::Scope p("normalize", s);
+      dim3 g(ny, kSegs);
+      k_normalize<<<g, kThreads, 0, s>>>(in, y0, nb, userHist ? hist_dev : partHist.data(),
+                                         userHist ? 1u : chunks, pb, table.data(), pdf.data(),
+                                         rawCk ? partCk.data() : nullptr, ck.data());
+      HIP_LAUNCH_CHECK();
+    }
+    if (MB > 0) {
+      prof::Scope p("encode", s);
+      dim3 g(divUp(MB, kBlocksPerWG), ny);
+      k_encode<FT><<<g, kThreads, 0, s>>>(in, out, y0, nb, MB, table.data(), slots.data(),
+                                          cw.data());
+      HIP_LAUNCH_CHECK();
+    }
+    {
+      prof::Scope p("coalesce", s);
+      const uint32_t bpw = 32;
+      dim3 g(std::max(1u, divUp(MB, bpw)), ny, kSegs);
+      k_coalesce<FT><<<g, kThreads, 0, s>>>(in, out, y0, nb, std::max(MB, 1u), bpw, slots.data(),
+                                            cw.data(), pdf.data(), pb, useChecksum, ck.data(),
+                                            outSize_dev);
+      HIP_LAUNCH_CHECK();
+    }
+  }
+}
+
+template <int FT>
+void decodeBatchDevice(StackDeviceMemory& res, int pb, uint32_t nb, const BatchDesc& in,
+                       const BatchDesc& out, uint32_t maxCapacity, uint8_t* outSuccess_dev,
+                       uint32_t* outSize_dev, hipStream_t s) {
+  checkProbBits(pb);
+  if (nb == 0) return;
+  const uint32_t maxBlocks = divUp(maxCapacity, kBlockSize);
+  for (uint32_t y0 = 0; y0 < nb; y0 += kMaxGridY) {
+    const uint32_t ny = std::min(kMaxGridY, nb - y0);
+    prof::Scope p("decode", s);
+    dim3 g(std::max(1u, divUp(maxBlocks, kBlocksPerWG)), ny);
+    k_decode<FT><<<g, kThreads, 0, s>>>(in, out, y0, pb, outSuccess_dev, outSize_dev);
+    HIP_LAUNCH_CHECK();
+  }
+}
+
+// Verify stored checksums against `unitBytes * out.size(b)` decoded bytes
+// (ansDecodeBatch :557-591 / floatDecompressDevice :1077-1112).  Host sync.
+std::vector<std::pair<int, std::string>> verifyChecksums(StackDeviceMemory& res, uint32_t nb,
+                                                         const BatchDesc& archives, bool isFloat,
+                                                         const BatchDesc& decoded,
+                                                         uint32_t maxBytes, hipStream_t s) {
+  std::vector<std::pair<int, std::string>> errs;
+  if (nb == 0) return errs;
+  auto now = res.alloc<uint32_t>(s, nb);
+  auto old = res.alloc<uint32_t>(s, nb);
+  HIP_CHECK(hipMemsetAsync(now.data(), 0, sizeof(uint32_t) * nb, s));
+  const uint32_t ckChunk = 1u << 20;
+  for (uint32_t y0 = 0; y0 < nb; y0 += kMaxGridY) {
+    const uint32_t ny = std::min(kMaxGridY, nb - y0);
+    dim3 g(std::max(1u, divUp(maxBytes, ckChunk)), ny);
+    k_checksum<<<g, kThreads, 0, s>>>(decoded, y0, 1, ckChunk, now.data());
+    HIP_LAUNCH_CHECK();
+  }
+  k_info<<<divUp(nb, 128), 128, 0, s>>>(archives, nb, isFloat, nullptr, nullptr, old.data());
+  HIP_LAUNCH_CHECK();
+  auto a = now.copyToHost(s);
+  auto o = old.copyToHost(s);
+  for (uint32_t i = 0; i < nb; ++i) {
+    if (a[i] != o[i]) {
+      std::ostringstream e;
+      e << "Checksum mismatch in batch member " << i << ": expected checksum " << std::hex << o[i]
+        << " got " << a[i] << "\n";
+      errs.emplace_back(int(i), e.str());
+    }
+  }
+  return errs;
+}
+
+// ---------------------------------------------------------------------------
+// parameter tables (one pinned H2D copy per call)
+// ---------------------------------------------------------------------------
+struct DeviceTables {
+  GpuMemoryReservation<uint8_t> mem;
+  const uint64_t* u64a = nullptr;
+  const uint64_t* u64b = nullptr;
+  const uint32_t* u32a = nullptr;
+};
+
+DeviceTables uploadTables(StackDeviceMemory& res, hipStream_t s, uint32_t nb,
+                          const std::vector<uint64_t>& a, const std::vector<uint64_t>& b,
+                          const std::vector<uint32_t>& c) {
+  const size_t bytesA = a.size() * 8, bytesB = b.size() * 8, bytesC = c.size() * 4;
+  std::vector<uint8_t> host(bytesA + bytesB + bytesC);
+  if (bytesA) std::memcpy(host.data(), a.data(), bytesA);
+  if (bytesB) std::memcpy(host.data() + bytesA, b.data(), bytesB);
+  if (bytesC) std::memcpy(host.data() + bytesA + bytesB, c.data(), bytesC);
+  DeviceTables t;
+  t.mem = res.alloc<uint8_t>(s, std::max<size_t>(host.size(), 1));
+  StackDeviceMemory::copyToDevice(t.mem.data(), host.data(), host.size(), s);
+  t.u64a = reinterpret_cast<const uint64_t*>(t.mem.data());
+  t.u64b = reinterpret_cast<const uint64_t*>(t.mem.data() + bytesA);
+  t.u32a = reinterpret_cast<const uint32_t*>(t.mem.data() + bytesA + bytesB);
+  (void)nb;
+  return t;
+}
+
+static void checkOutAligned(const void* p, const char* what) {
+  DG_CHECK(reinterpret_cast<uintptr_t>(p) % 16 == 0,
+           what << " must be 16-byte aligned (archives are written with 16 B stores)");
+}
+
+// ---------------------------------------------------------------------------
+// ANS byte codec API
+// ---------------------------------------------------------------------------
+uint32_t getMaxCompressedSize(uint32_t bytes) {
+  // ans/GpuANSEncode.cu:13-25 (overhead term evaluated for 4096 *blocks*)
+  uint64_t raw = ansOverhead(kBlockSize);
+  raw += uint64_t(roundUp(kBlockSize + kBlockSize / 4, 16)) * divUp(bytes, kBlockSize);
+  raw = roundUp64(raw, 16);
+  DG_CHECK(raw <= uint64_t(INT32_MAX), "input too large: " << bytes << " bytes");
+  return uint32_t(raw);
+}
+
+void ansEncodeBatchStride(StackDeviceMemory& res, const ANSCodecConfig& config,
+                          uint32_t numInBatch, const void* in_dev, uint32_t inPerBatchSize,
+                          uint32_t inPerBatchStride, const uint32_t* histogram_dev,
+                          void* out_dev, uint32_t outPerBatchStride,
+                          uint32_t* outBatchSize_dev, hipStream_t stream) {
+  if (numInBatch == 0) return;
+  checkOutAligned(out_dev, "out_dev");
+  DG_CHECK(outPerBatchStride % 16 == 0, "outPerBatchStride must be a multiple of 16");
+  auto in = BatchDesc::strided(in_dev, inPerBatchStride, inPerBatchSize);
+  auto out = BatchDesc::strided(out_dev, outPerBatchStride, 0);
+  encodeBatchDevice<0>(res, config.probBits, config.useChecksum, numInBatch, in, inPerBatchSize,
+                       histogram_dev, out, outBatchSize_dev, stream);
+}
+
+void ansEncodeBatchPointer(StackDeviceMemory& res, const ANSCodecConfig& config,
+                           uint32_t numInBatch, const void** in, const uint32_t* inSize,
+                           const uint32_t* histogram_dev, void** out, uint32_t* outSize_dev,
+                           hipStream_t stream) {
+  if (numInBatch == 0) return;
+  std::vector<uint64_t> ip(numInBatch), op(numInBatch);
+  std::vector<uint32_t> sz(numInBatch);
+  uint32_t maxSize = 0;
+  for (uint32_t i = 0; i < numInBatch; ++i) {
+    ip[i] = reinterpret_cast<uint64_t>(in[i]);
+    op[i] = reinterpret_cast<uint64_t>(out[i]);
+    checkOutAligned(out[i], "out[i]");
+    sz[i] = inSize[i];
+    maxSize = std::max(maxSize, inSize[i]);
+  }
+  auto t = uploadTables(res, stream, numInBatch, ip, op, sz);
+  auto inD = BatchDesc::pointers(t.u64a, t.u32a);
+  auto outD = BatchDesc::pointers(t.u64b, nullptr);
+  encodeBatchDevice<0>(res, config.probBits, config.useChecksum, numInBatch, inD, maxSize,
+                       histogram_dev, outD, outSize_dev, stream);
+}
+
+void ansEncodeBatchSplitSize(StackDeviceMemory& res, const ANSCodecConfig& config,
+                             uint32_t numInBatch, const void* in_dev,
+                             const uint32_t* inSplitSizes, const uint32_t* histogram_dev,
+                             void* out_dev, uint32_t outStride, uint32_t* outSize_dev,
+                             hipStream_t stream) {
+  if (numInBatch == 0) return;
+  DG_CHECK(reinterpret_cast<uintptr_t>(in_dev) % kANSRequiredAlignment == 0,
+           "in_dev must be " << kANSRequiredAlignment << "-byte aligned");
+  checkOutAligned(out_dev, "out_dev");
+  DG_CHECK(outStride % 16 == 0, "outStride must be a multiple of 16");
+  std::vector<uint64_t> off(numInBatch);
+  std::vector<uint32_t> sz(numInBatch);
+  uint64_t run = 0;
+  uint32_t maxSize = 0;
+  for (uint32_t i = 0; i < numInBatch; ++i) {
+    if (i + 1 != numInBatch) {
+      DG_CHECK(inSplitSizes[i] % kANSRequiredAlignment == 0,
+               "interior split sizes must be multiples of " << kANSRequiredAlignment);
+    }
+    off[i] = run;
+    sz[i] = inSplitSizes[i];
+    run += inSplitSizes[i];
+    maxSize = std::max(maxSize, inSplitSizes[i]);
+  }
+  auto t = uploadTables(res, stream, numInBatch, off, {}, sz);
+  auto inD = BatchDesc::split(in_dev, t.u64a, t.u32a);
+  auto outD = BatchDesc::strided(out_dev, outStride, 0);
+  encodeBatchDevice<0>(res, config.probBits, config.useChecksum, numInBatch, inD, maxSize,
+                       histogram_dev, outD, outSize_dev, stream);
+}
+
+static ANSDecodeStatus ansDecodeCommon(StackDeviceMemory& res, const ANSCodecConfig& config,
+                                       uint32_t nb, const BatchDesc& in, const BatchDesc& out,
+                                       uint32_t maxCap, uint8_t* succ, uint32_t* sizes,
+                                       hipStream_t s) {
+  ANSDecodeStatus status;
+  decodeBatchDevice<0>(res, config.probBits, nb, in, out, maxCap, succ, sizes, s);
+  if (config.useChecksum) {
+    status.errorInfo = verifyChecksums(res, nb, in, false, out, maxCap, s);
+    if (!status.errorInfo.empty()) status.error = ANSDecodeError::ChecksumMismatch;
+  }
+  return status;
+}
+
+ANSDecodeStatus ansDecodeBatchStride(StackDeviceMemory& res, const ANSCodecConfig& config,
+                                     uint32_t numInBatch, const void* in_dev,
+                                     uint32_t inPerBatchStride, void* out_dev,
+                                     uint32_t outPerBatchStride, uint32_t outPerBatchCapacity,
+                                     uint8_t* outSuccess_dev, uint32_t* outSize_dev,
+                                     hipStream_t stream) {
+  if (numInBatch == 0) return ANSDecodeStatus();
+  auto in = BatchDesc::strided(in_dev, inPerBatchStride, 0);
+  auto out = BatchDesc::strided(out_dev, outPerBatchStride, outPerBatchCapacity);
+  return ansDecodeCommon(res, config, numInBatch, in, out, outPerBatchCapacity, outSuccess_dev,
+                         outSize_dev, stream);
+}
+
+ANSDecodeStatus ansDecodeBatchPointer(StackDeviceMemory& res, const ANSCodecConfig& config,
+                                      uint32_t numInBatch, const void** in, void** out,
+                                      const uint32_t* outCapacity, uint8_t* outSuccess_dev,
+                                      uint32_t* outSize_dev, hipStream_t stream) {
+  if (numInBatch == 0) return ANSDecodeStatus();
+  std::vector<uint64_t> ip(numInBatch), op(numInBatch);
+  std::vector<uint32_t> cap(numInBatch);
+  uint32_t maxCap = 0;
+  for (uint32_t i = 0; i < numInBatch; ++i) {
+    ip[i] = reinterpret_cast<uint64_t>(in[i]);
+    op[i] = reinterpret_cast<uint64_t>(out[i]);
+    cap[i] = outCapacity[i];
+    maxCap = std::max(maxCap, cap[i]);
+  }
+  auto t = uploadTables(res, stream, numInBatch, ip, op, cap);
+  auto inD = BatchDesc::pointers(t.u64a, nullptr);
+  auto outD = BatchDesc::pointers(t.u64b, t.u32a);
+  return ansDecodeCommon(res, config, numInBatch, inD, outD, maxCap, outSuccess_dev, outSize_dev,
+                         stream);
+}
+
+ANSDecodeStatus ansDecodeBatchSplitSize(StackDeviceMemory& res, const ANSCodecConfig& config,
+                                        uint32_t numInBatch, const void** in, void* out_dev,
+                                        const uint32_t* outSplitSizes, uint8_t* outSuccess_dev,
+                                        uint32_t* outSize_dev, hipStream_t stream) {
+  if (numInBatch == 0) return ANSDecodeStatus();
+  DG_CHECK(reinterpret_cast<uintptr_t>(out_dev) % kANSRequiredAlignment == 0,
+           "out_dev must be " << kANSRequiredAlignment << "-byte aligned");
+  std::vector<uint64_t> ip(numInBatch), off(numInBatch);
+  std::vector<uint32_t> sz(numInBatch);
+  uint64_t run = 0;
+  uint32_t maxCap = 0;
+  for (uint32_t i = 0; i < numInBatch; ++i) {
+    if (i + 1 != numInBatch) {
+      DG_CHECK(outSplitSizes[i] % kANSRequiredAlignment == 0,
+               "interior split sizes must be multiples of " << kANSRequiredAlignment);
+    }
+    ip[i] = reinterpret_cast<uint64_t>(in[i]);
+    off[i] = run;
+    sz[i] = outSplitSizes[i];
+    run += outSplitSizes[i];
+    maxCap = std::max(maxCap, sz[i]);
+  }
+  auto t = uploadTables(res, stream, numInBatch, ip, off, sz);
+  auto inD = BatchDesc::pointers(t.u64a, nullptr);
+  auto outD = BatchDesc::split(out_dev, t.u64b, t.u32a);
+  return ansDecodeCommon(res, config, numInBatch, inD, outD, maxCap, outSuccess_dev, outSize_dev,
+                         stream);
+}
+
+void ansGetCompressedInfoDevice(StackDeviceMemory& res, const void** in_dev, uint32_t numInBatch,
+                                uint32_t* outSizes_dev, uint32_t* outChecksum_dev,
+                                hipStream_t stream) {
+  if (numInBatch == 0 || (!outSizes_dev && !outChecksum_dev)) return;
+  auto inD = BatchDesc::pointers(reinterpret_cast<const uint64_t*>(in_dev), nullptr);
+  k_info<<<divUp(numInBatch, 128), 128, 0, stream>>>(inD, numInBatch, false, outSizes_dev,
+                                                      nullptr, outChecksum_dev);
+  HIP_LAUNCH_CHECK();
+}
+
+void ansGetCompressedInfo(StackDeviceMemory& res, const void** in, uint32_t numInBatch,
+                          uint32_t* outSizes_dev, uint32_t* outChecksum_dev, hipStream_t stream) {
+  if (numInBatch == 0 || (!outSizes_dev && !outChecksum_dev)) return;
+  std::vector<uint64_t> ip(numInBatch);
+  for (uint32_t i = 0; i < numInBatch; ++i) ip[i] = reinterpret_cast<uint64_t>(in[i]);
+  auto t = uploadTables(res, stream, numInBatch, ip, {}, {});
+  ansGetCompressedInfoDevice(res, reinterpret_cast<const void**>(const_cast<uint64_t*>(t.u64a)),
+                             numInBatch, outSizes_dev, outChecksum_dev, stream);
+}
+
+// ---------------------------------------------------------------------------
+// float codec API
+// ---------------------------------------------------------------------------
+uint32_t getMaxFloatCompressedSize(FloatType ft, uint32_t size) {
+  DG_CHECK(ft != FloatType::kUndefined && uint32_t(ft) <= 4, "bad float type");
+  uint64_t base = 32ull + getMaxCompressedSize(size) + floatRawBytes(int(ft), size);
+  if (ft == FloatType::kFloat64) base += getMaxCompressedSize(size);
+  return uint32_t(base);
+}
+
+static void checkFloatConfig(const FloatCodecConfig& c) {
+  DG_CHECK(!c.ansConfig.useChecksum,
+           "ANS-level checksumming is not allowed in float mode (use FloatCodecConfig.useChecksum)");
+  DG_CHECK(c.floatType != FloatType::kUndefined && uint32_t(c.floatType) <= 4, "bad float type");
+}
+
+void floatCompressDescs(StackDeviceMemory& res, const FloatCompressConfig& config, uint32_t nb,
+                        const BatchDesc& in, uint32_t maxSize, const BatchDesc& out,
+                        uint32_t* outSize_dev, hipStream_t s) {
+  checkFloatConfig(config);
+  const int pb = config.ansConfig.probBits;
+  switch (config.floatType) {
+    case FloatType::kFloat16:
+      encodeBatchDevice<1>(res, pb, config.useChecksum, nb, in, maxSize, nullptr, out, outSize_dev, s);
+      break;
+    case FloatType::kBFloat16:
+      encodeBatchDevice<2>(res, pb, config.useChecksum, nb, in, maxSize, nullptr, out, outSize_dev, s);
+      break;
+    case FloatType::kFloat32:
+      encodeBatchDevice<3>(res, pb, config.useChecksum, nb, in, maxSize, nullptr, out, outSize_dev, s);
+      break;
+    default:
+      encodeBatchDevice<4>(res, pb, config.useChecksum, nb, in, maxSize, nullptr, out, outSize_dev, s);
+      break;
+  }
+}
+
+FloatDecompressStatus floatDecompressDescs(StackDeviceMemory& res,
+                                           const FloatDecompressConfig& config, uint32_t nb,
+                                           const BatchDesc& in, const BatchDesc& out,
+                                           uint32_t maxCap, uint8_t* succ, uint32_t* sizes,
+                                           hipStream_t s) {
+  checkFloatConfig(config);
+  const int pb = config.ansConfig.probBits;
+  switch (config.floatType) {
+    case FloatType::kFloat16:
+      decodeBatchDevice<1>(res, pb, nb, in, out, maxCap, succ, sizes, s);
+      break;
+    case FloatType::kBFloat16:
+      decodeBatchDevice<2>(res, pb, nb, in, out, maxCap, succ, sizes, s);
+      break;
+    case FloatType::kFloat32:
+      decodeBatchDevice<3>(res, pb, nb, in, out, maxCap, succ, sizes, s);
+      break;
+    default:
+      decodeBatchDevice<4>(res, pb, nb, in, out, maxCap, succ, sizes, s);
+      break;
+  }
+  FloatDecompressStatus status;
+  if (config.useChecksum) {
+    // checksums `capacity` bytes (float words treated as bytes), as the
+    // reference does (float/GpuFloatDecompress.cuh:1077-1112)
+    status.errorInfo = verifyChecksums(res, nb, in, true, out, maxCap, s);
+    if (!status.errorInfo.empty()) status.error = FloatDecompressError::ChecksumMismatch;
+  }
+  return status;
+}
+
+void floatCompress(StackDeviceMemory& res, const FloatCompressConfig& config, uint32_t numInBatch,
+                   const void** in, const uint32_t* inSize, void** out, uint32_t* outSize_dev,
+                   hipStream_t stream) {
+  if (numInBatch == 0) return;
+  checkFloatConfig(config);
+  const uint32_t ws = floatWordBytes(int(config.floatType));
+  std::vector<uint64_t> ip(numInBatch), op(numInBatch);
+  std::vector<uint32_t> sz(numInBatch);
+  uint32_t maxSize = 0;
+  for (uint32_t i = 0; i < numInBatch; ++i) {
+    ip[i] = reinterpret_cast<uint64_t>(in[i]);
+    op[i] = reinterpret_cast<uint64_t>(out[i]);
+    DG_CHECK(ip[i] % ws == 0, "float input " << i << " not aligned to its word size");
+    checkOutAligned(out[i], "out[i]");
+    sz[i] = inSize[i];
+    maxSize = std::max(maxSize, inSize[i]);
+  }
+  auto t = uploadTables(res, stream, numInBatch, ip, op, sz);
+  floatCompressDescs(res, config, numInBatch, BatchDesc::pointers(t.u64a, t.u32a), maxSize,
+                     BatchDesc::pointers(t.u64b, nullptr), outSize_dev, stream);
+}
+
+void floatCompressSplitSize(StackDeviceMemory& res, const FloatCompressConfig& config,
+                            uint32_t numInBatch, const void* in_dev, const uint32_t* inSplitSizes,
+                            void* out_dev, uint32_t outStride, uint32_t* outSize_dev,
+                            hipStream_t stream) {
+  if (numInBatch == 0) return;
+  checkFloatConfig(config);
+  checkOutAligned(out_dev, "out_dev");
+  DG_CHECK(outStride % 16 == 0, "outStride must be a multiple of 16");
+  const uint32_t ws = floatWordBytes(int(config.floatType));
+  DG_CHECK(reinterpret_cast<uintptr_t>(in_dev) % ws == 0, "in_dev not word aligned");
+  std::vector<uint64_t> off(numInBatch);
+  std::vector<uint32_t> sz(numInBatch);
+  uint64_t run = 0;
+  uint32_t maxSize = 0;
+  for (uint32_t i = 0; i < numInBatch; ++i) {
+    off[i] = run * ws;
+    sz[i] = inSplitSizes[i];
+    run += inSplitSizes[i];
+    maxSize = std::max(maxSize, sz[i]);
+  }
+  auto t = uploadTables(res, stream, numInBatch, off, {}, sz);
+  floatCompressDescs(res, config, numInBatch, BatchDesc::split(in_dev, t.u64a, t.u32a), maxSize,
+                     BatchDesc::strided(out_dev, outStride, 0), outSize_dev, stream);
+}
+
+void floatCompressBatchStride(StackDeviceMemory& res, const FloatCompressConfig& config,
+                              uint32_t numInBatch, const void* in_dev, uint32_t inPerBatchWords,
+                              uint64_t inPerBatchStrideBytes, void* out_dev,
+                              uint64_t outPerBatchStrideBytes, uint32_t* outSize_dev,
+                              hipStream_t stream) {
+  if (numInBatch == 0) return;
+  checkOutAligned(out_dev, "out_dev");
+  DG_CHECK(outPerBatchStrideBytes % 16 == 0, "out stride must be a multiple of 16");
+  floatCompressDescs(res, config, numInBatch,
+                     BatchDesc::strided(in_dev, inPerBatchStrideBytes, inPerBatchWords),
+                     inPerBatchWords, BatchDesc::strided(out_dev, outPerBatchStrideBytes, 0),
+                     outSize_dev, stream);
+}
+
+FloatDecompressStatus floatDecompress(StackDeviceMemory& res, const FloatDecompressConfig& config,
+                                      uint32_t numInBatch, const void** in, void** out,
+                                      const uint32_t* outCapacity, uint8_t* outSuccess_dev,
+                                      uint32_t* outSize_dev, hipStream_t stream) {
+  if (numInBatch == 0) return FloatDecompressStatus();
+  checkFloatConfig(config);
+  const uint32_t ws = floatWordBytes(int(config.floatType));
+  std::vector<uint64_t> ip(numInBatch), op(numInBatch);
+  std::vector<uint32_t> cap(numInBatch);
+  uint32_t maxCap = 0;
+  for (uint32_t i = 0; i < numInBatch; ++i) {
+    ip[i] = reinterpret_cast<uint64_t>(in[i]);
+    op[i] = reinterpret_cast<uint64_t>(out[i]);
+    DG_CHECK(op[i] % ws == 0, "float output " << i << " not aligned to its word size");
+    cap[i] = outCapacity[i];
+    maxCap = std::max(maxCap, cap[i]);
+  }
+  auto t = uploadTables(res, stream, numInBatch, ip, op, cap);
+  return floatDecompressDescs(res, config, numInBatch, BatchDesc::pointers(t.u64a, nullptr),
+                              BatchDesc::pointers(t.u64b, t.u32a), maxCap, outSuccess_dev,
+                              outSize_dev, stream);
+}
+
+FloatDecompressStatus floatDecompressSplitSize(StackDeviceMemory& res,
+                                               const FloatDecompressConfig& config,
+                                               uint32_t numInBatch, const void** in, void* out_dev,
+                                               const uint32_t* outSplitSizes,
+                                               uint8_t* outSuccess_dev, uint32_t* outSize_dev,
+                                               hipStream_t stream) {
+  if (numInBatch == 0) return FloatDecompressStatus();
+  checkFloatConfig(config);
+  const uint32_t ws = floatWordBytes(int(config.floatType));
+  DG_CHECK(reinterpret_cast<uintptr_t>(out_dev) % ws == 0, "out_dev not word aligned");
+  std::vector<uint64_t> ip(numInBatch), off(numInBatch);
+  std::vector<uint32_t> sz(numInBatch);
+  uint64_t run = 0;
+  uint32_t maxCap = 0;
+  for (uint32_t i = 0; i < numInBatch; ++i) {
+    ip[i] = reinterpret_cast<uint64_t>(in[i]);
+    off[i] = run * ws;
+    sz[i] = outSplitSizes[i];
+    run += outSplitSizes[i];
+    maxCap = std::max(maxCap, sz[i]);
+  }
+  auto t = uploadTables(res, stream, numInBatch, ip, off, sz);
+  return floatDecompressDescs(res, config, numInBatch, BatchDesc::pointers(t.u64a, nullptr),
+                              BatchDesc::split(out_dev, t.u64b, t.u32a), maxCap, outSuccess_dev,
+                              outSize_dev, stream);
+}
+
+FloatDecompressStatus floatDecompressBatchStride(StackDeviceMemory& res,
+                                                 const FloatDecompressConfig& config,
+                                                 uint32_t numInBatch, const void* in_dev,
+                                                 uint64_t inPerBatchStrideBytes, void* out_dev,
+                                                 uint64_t outPerBatchStrideBytes,
+                                                 uint32_t outPerBatchCapacityWords,
+                                                 uint8_t* outSuccess_dev, uint32_t* outSize_dev,
+                                                 hipStream_t stream) {
+  if (numInBatch == 0) return FloatDecompressStatus();
+  return floatDecompressDescs(
+      res, config, numInBatch, BatchDesc::strided(in_dev, inPerBatchStrideBytes, 0),
+      BatchDesc::strided(out_dev, outPerBatchStrideBytes, outPerBatchCapacityWords),
+      outPerBatchCapacityWords, outSuccess_dev, outSize_dev, stream);
+}
+
+void floatGetCompressedInfoDevice(StackDeviceMemory& res, const void** in_dev, uint32_t numInBatch,
+                                  uint32_t* outSizes_dev, uint32_t* outTypes_dev,
+                                  uint32_t* outChecksum_dev, hipStream_t stream) {
+  if (numInBatch == 0 || (!outSizes_dev && !outTypes_dev && !outChecksum_dev)) return;
+  auto inD = BatchDesc::pointers(reinterpret_cast<const uint64_t*>(in_dev), nullptr);
+  k_info<<<divUp(numInBatch, 128), 128, 0, stream>>>(inD, numInBatch, true, outSizes_dev,
+                                                      outTypes_dev, outChecksum_dev);
+  HIP_LAUNCH_CHECK();
+}
+
+void floatGetCompressedInfo(StackDeviceMemory& res, const void** in, uint32_t numInBatch,
+                            uint32_t* outSizes_dev, uint32_t* outTypes_dev,
+                            uint32_t* outChecksum_dev, hipStream_t stream) {
+  if (numInBatch == 0 || (!outSizes_dev && !outTypes_dev && !outChecksum_dev)) return;
+  std::vector<uint64_t> ip(numInBatch);
+  for (uint32_t i = 0; i < numInBatch; ++i) ip[i] = reinterpret_cast<uint64_t>(in[i]);
+  auto t = uploadTables(res, stream, numInBatch, ip, {}, {});
+  floatGetCompressedInfoDevice(res, reinterpret_cast<const void**>(const_cast<uint64_t*>(t.u64a)),
+                               numInBatch, outSizes_dev, outTypes_dev, outChecksum_dev, stream);
+}
+
+}  // namespace dietgpu

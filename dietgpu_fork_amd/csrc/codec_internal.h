@@ -1,0 +1,30 @@
+// Internal entry points shared by the dense and sparse float drivers.
+#pragma once
+
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "batch.h"
+#include "dietgpu/GpuFloatCodec.h"
+
+namespace dietgpu {
+
+void floatCompressDescs(StackDeviceMemory& res, const FloatCompressConfig& config, uint32_t nb,
+                        const BatchDesc& in, uint32_t maxSize, const BatchDesc& out,
+                        uint32_t* outSize_dev, hipStream_t s);
+
+FloatDecompressStatus floatDecompressDescs(StackDeviceMemory& res,
+                                           const FloatDecompressConfig& config, uint32_t nb,
+                                           const BatchDesc& in, const BatchDesc& out,
+                                           uint32_t maxCap, uint8_t* succ, uint32_t* sizes,
+                                           hipStream_t s);
+
+// Compare archive checksums with the XOR of `decoded.size(b)` bytes of each
+// decoded element; synchronises `s`.
+std::vector<std::pair<int, std::string>> verifyChecksums(StackDeviceMemory& res, uint32_t nb,
+                                                         const BatchDesc& archives, bool isFloat,
+                                                         const BatchDesc& decoded,
+                                                         uint32_t maxBytes, hipStream_t s);
+
+}  // namespace dietgpu
