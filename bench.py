@@ -1,0 +1,209 @@
+"""Benchmark: encode+decode GB/s of the bf16 float codec on MI355X.
+
+Workload (BASELINE.json configs[1], "c2"): per GPU a batch of 256 x 1 MiB
+bf16 tensors (524,288 words each), N(0,1) fp32 truncated to bf16, seeded.
+One step = floatCompress (pointer API, the reference's drop-in path) ->
+RCCL all-gather of the per-tensor compressed sizes (N > 1) -> floatDecompress.
+Weak scaling: every rank processes its own 256-tensor shard.
+
+value = N * U / step_time  (U = 256 MiB of uncompressed input per rank,
+GB/s = 1e9 B/s, reference convention benchmark.py:158-159).
+
+Run:  python bench.py [--gpus N --steps K --warmup W]
+      torchrun --nproc-per-node N bench.py --gpus N ...
+"""
+import argparse
+import ctypes
+import glob
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+METRIC = "encode+decode GB/s (+ratio) on bf16 batch at 1/2/4/8 MI355X vs HBM roofline"
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--batch", type=int, default=256)
+    p.add_argument("--words", type=int, default=524288)
+    p.add_argument("--prob-bits", type=int, default=10)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-sample", type=int, default=256,
+                   help="tensors of the batch timed on the CPU oracle (rank 0, N=1)")
+    p.add_argument("--verify", action="store_true", default=True)
+    return p.parse_args()
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    import dietgpu_fork_amd  # noqa: F401
+    from dietgpu_fork_amd import _native as N
+    from dietgpu_fork_amd import codec as C
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world and world == 1 and args.gpus > 1:
+        raise SystemExit("--gpus > 1 must be launched with torch.distributed.run (one rank/GPU)")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    nb, n, pb = args.batch, args.words, args.prob_bits
+    U = nb * n * 2  # bytes per rank
+    g = torch.Generator(device=dev).manual_seed(1000 + rank)
+    x32 = torch.randn(nb, n, generator=g, device=dev, dtype=torch.float32)
+    x = (x32.view(torch.int32) >> 16).to(torch.int16).view(torch.bfloat16)  # truncation
+    del x32
+    L = N.lib()
+    ft = 2
+    cols = L.dietgpu_get_max_float_compressed_size(ft, n)
+    comp = torch.empty([nb, cols], dtype=torch.uint8, device=dev)
+    sizes = torch.empty([nb], dtype=torch.int32, device=dev)
+    out = torch.empty_like(x)
+    ok = torch.empty([nb], dtype=torch.uint8, device=dev)
+    osz = torch.empty([nb], dtype=torch.int32, device=dev)
+    ws = C.Workspace(768 << 20, dev)
+    gathered = torch.empty([nb * world], dtype=torch.int32, device=dev)
+
+    in_ptrs = N.ptr_array([x.data_ptr() + i * n * 2 for i in range(nb)])
+    in_size = N.u32_array([n] * nb)
+    comp_ptrs = N.ptr_array([comp.data_ptr() + i * cols for i in range(nb)])
+    out_ptrs = N.ptr_array([out.data_ptr() + i * n * 2 for i in range(nb)])
+    caps = N.u32_array([n] * nb)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+
+    def step():
+        N.check(L.dietgpu_float_compress(ws.h, ft, pb, 0, nb, in_ptrs, in_size, comp_ptrs,
+                                         sizes.data_ptr(), stream))
+        if world > 1:
+            dist.all_gather_into_tensor(gathered, sizes)
+        N.check(L.dietgpu_float_decompress(ws.h, ft, pb, 0, nb, comp_ptrs, out_ptrs, caps,
+                                           ok.data_ptr(), osz.data_ptr(), stream))
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if args.verify:
+        assert bool((ok == 1).all()), "decode reported failure"
+        assert torch.equal(out.view(torch.int16), x.view(torch.int16)), "roundtrip mismatch"
+    comp_bytes = int(sizes.to(torch.int64).sum().item())
+
+    # timed region: barrier + sync on both sides, K steps, max over ranks
+    C.profile_reset()
+    C.profile(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    C.profile(False)
+    elapsed = t1 - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        cb = torch.tensor([comp_bytes], dtype=torch.int64, device=dev)
+        dist.all_reduce(cb)
+        comp_total = int(cb.item())
+    else:
+        comp_total = comp_bytes
+    ms_per_step = elapsed / args.steps * 1e3
+    value = world * U * args.steps / elapsed / 1e9
+
+    # per-kernel-family device time (hipEvents on the launch stream)
+    fam = {}
+    for k in ("hist", "normalize", "encode", "coalesce", "decode"):
+        ms, launches = C.profile_query(k)
+        if launches:
+            fam[k] = {"avg_ms": ms / launches, "launches": launches}
+    # algorithmic bytes per launch (Measurement): one launch covers
+    # the whole batch; C = compressed bytes (raw section + ANS), U = input.
+    algo = {"decode": U + comp_bytes, "encode": U + comp_bytes, "hist": U,
+            "coalesce": 2 * max(comp_bytes - U // 2, 0), "normalize": 0}
+    dominant = max(fam, key=lambda k: fam[k]["avg_ms"]) if fam else None
+    roofline = None
+    if dominant:
+        ach = algo[dominant] / (fam[dominant]["avg_ms"] * 1e-3) / 1e9
+        roofline = {"bound": "hbm", "kernel": f"k_{dominant}", "achieved": round(ach, 1),
+                    "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBPS, 4),
+                    "traffic": _pmc_traffic(dominant, U, comp_bytes),
+                    "algorithmic_bytes_per_launch": algo[dominant]}
+    t_enc = sum(fam[k]["avg_ms"] for k in ("hist", "normalize", "encode", "coalesce") if k in fam)
+    t_dec = fam.get("decode", {}).get("avg_ms", 0.0)
+    line = {
+        "metric": METRIC, "value": round(value, 2), "unit": "GB/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+        "data": "synthetic",
+        "config": {"workload": f"c2: batch={nb} x {n * 2 // 1048576} MiB bf16 N(0,1) per GPU",
+                   "batch_per_gpu": nb, "words_per_tensor": n, "prob_bits": pb,
+                   "api": "floatCompress + floatDecompress (pointer API, C ABI)",
+                   "parallelism": f"dp{world} (independent shards + RCCL size all-gather)"},
+        "ratio": round(comp_total / (world * U), 5),
+        "encode_plus_decode_algorithmic_GBps": (round(2 * (U + comp_bytes) / ((t_enc + t_dec) * 1e-3) / 1e9, 1)
+                                                if t_enc and t_dec else None),
+        "compress_GBps_kernels": round(U / (t_enc * 1e-3) / 1e9, 1) if t_enc else None,
+        "decompress_GBps_kernels": round(U / (t_dec * 1e-3) / 1e9, 1) if t_dec else None,
+        "kernels": {k: round(v["avg_ms"], 5) for k, v in fam.items()},
+        "roofline": roofline,
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = _cpu_baseline(x, min(args.cpu_sample, nb), pb)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def _pmc_traffic(kernel, U, comp):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC
+    summary (profiles/*pmc*.json, written by tools/pmc_summary.py), or None."""
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")))
+    for f in reversed(files):
+        try:
+            d = json.load(open(f))
+        except Exception:
+            continue
+        k = d.get("kernels", {}).get("k_" + kernel)
+        if k and "hbm_bytes_per_launch" in k:
+            return k["hbm_bytes_per_launch"]
+    return None
+
+
+def _cpu_baseline(x, sample, pb):
+    import numpy as np
+    import torch
+
+    from oracle import oracle as O
+
+    words = x[:sample].view(torch.int16).cpu().numpy().view(np.uint16)
+    t, comp, te, td = O.time_float_roundtrip(words, 2, pb, threads=1)
+    U = words.nbytes
+    return {"value": round(U / t / 1e9, 4), "unit": "GB/s", "cores": 1, "kind": "port",
+            "sample": f"{sample} x {words.shape[1] * 2 // 1048576} MiB bf16 of the c2 batch, "
+                      f"1 pass compress+decompress, serial C oracle (oracle/dietgpu_oracle.c)",
+            "seconds": round(t, 3), "compress_s": round(te, 3), "decompress_s": round(td, 3),
+            "ratio": round(comp / U, 5), "host_cpus": os.cpu_count()}
+
+
+if __name__ == "__main__":
+    main()

@@ -16,7 +16,8 @@
 #include "codec_internal.h"
 #include "dietgpu/GpuANSCodec.h"
 #include "dietgpu/GpuFloatCodec.h"
-#include "kernels.h"
+#include "decode.h"
+#include "encode.h"
 #include "profile.h"
 
 namespace dietgpu {
@@ -97,8 +98,8 @@ void encodeBatchDevice(StackDeviceMemory& res, int pb, bool useChecksum, uint32_
     }
     if (MB > 0) {
       prof::Scope p("encode", s);
-      dim3 g(divUp(MB, kBlocksPerWG), ny);
-      k_encode<FT><<<g, kThreads, 0, s>>>(in, out, y0, nb, MB, table.data(), slots.data(),
+      dim3 g(divUp(MB, EncCfg<FT>::kBlocksPerWG), ny);
+      k_encode<FT><<<g, enc::kThreads, 0, s>>>(in, out, y0, nb, MB, table.data(), slots.data(),
                                           cw.data());
       HIP_LAUNCH_CHECK();
     }
@@ -124,8 +125,8 @@ void decodeBatchDevice(StackDeviceMemory& res, int pb, uint32_t nb, const BatchD
   for (uint32_t y0 = 0; y0 < nb; y0 += kMaxGridY) {
     const uint32_t ny = std::min(kMaxGridY, nb - y0);
     prof::Scope p("decode", s);
-    dim3 g(std::max(1u, divUp(maxBlocks, kBlocksPerWG)), ny);
-    k_decode<FT><<<g, kThreads, 0, s>>>(in, out, y0, pb, outSuccess_dev, outSize_dev);
+    dim3 g(std::max(1u, divUp(maxBlocks, DecCfg<FT>::kBlocksPerWG)), ny);
+    k_decode<FT><<<g, dec::kThreads, 0, s>>>(in, out, y0, pb, outSuccess_dev, outSize_dev);
     HIP_LAUNCH_CHECK();
   }
 }

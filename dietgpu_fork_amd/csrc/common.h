@@ -110,8 +110,10 @@ __device__ __forceinline__ uint32_t mbcnt(uint64_t mask) {
   return __builtin_amdgcn_mbcnt_hi(uint32_t(mask >> 32),
                                    __builtin_amdgcn_mbcnt_lo(uint32_t(mask), 0u));
 }
+// (HIP's __ballot(int) round-trips the predicate through a VGPR; the bool
+// builtin maps straight onto the compare's SGPR-pair result)
 __device__ __forceinline__ uint64_t ballot(bool p) {
-  return __ballot(p);
+  return __builtin_amdgcn_ballot_w64(p);
 }
 __device__ __forceinline__ uint32_t readfirst(uint32_t v) {
   return __builtin_amdgcn_readfirstlane(v);

@@ -1,0 +1,182 @@
+// Device-side building blocks shared by all kernels (gfx950 / wave64).
+#pragma once
+
+#include "batch.h"
+#include "common.h"
+
+namespace dietgpu {
+
+// Pointers into HBM carry address_space(1) so hipcc emits global_* (not
+// flat_*) memory instructions: flat ops count on both vmcnt and lgkmcnt and
+// force s_waitcnt vmcnt(0) lgkmcnt(0) at every LDS use.
+#define DG_G __attribute__((address_space(1)))
+template <typename T>
+using gp = DG_G T*;
+
+template <typename T>
+__device__ __forceinline__ gp<T> G(T* p) {
+  return (gp<T>)p;
+}
+
+__device__ __forceinline__ gp<uint8_t> startOf(const BatchDesc& d, uint32_t b) {
+  return G(d.start(b));
+}
+
+// 8 / 16-byte global accesses through native vector types (HIP's uint2 /
+// uint4 classes cannot bind address_space(1) references)
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint4 ld16(gp<const void> p) {
+  const u32x4 v = *(gp<const u32x4>)p;
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void st16(gp<void> p, uint4 v) {
+  *(gp<u32x4>)p = u32x4{v.x, v.y, v.z, v.w};
+}
+__device__ __forceinline__ uint2 ld8(gp<const void> p) {
+  const u32x2 v = *(gp<const u32x2>)p;
+  return make_uint2(v.x, v.y);
+}
+__device__ __forceinline__ void st8(gp<void> p, uint2 v) {
+  *(gp<u32x2>)p = u32x2{v.x, v.y};
+}
+
+template <int FT>
+struct FloatTraits;
+template <>
+struct FloatTraits<0> {  // raw bytes (ANS codec)
+  using WordT = uint8_t;
+  static constexpr int kSegs = 1;
+};
+template <>
+struct FloatTraits<1> {
+  using WordT = uint16_t;
+  static constexpr int kSegs = 1;
+};
+template <>
+struct FloatTraits<2> {
+  using WordT = uint16_t;
+  static constexpr int kSegs = 1;
+};
+template <>
+struct FloatTraits<3> {
+  using WordT = uint32_t;
+  static constexpr int kSegs = 1;
+};
+template <>
+struct FloatTraits<4> {
+  using WordT = uint64_t;
+  static constexpr int kSegs = 2;
+};
+
+__device__ __forceinline__ uint32_t rotl32(uint32_t v, int s) {
+  return (v << s) | (v >> (32 - s));
+}
+__device__ __forceinline__ uint32_t rotr32(uint32_t v, int s) {
+  return (v >> s) | (v << (32 - s));
+}
+__device__ __forceinline__ uint64_t rotl64(uint64_t v, int s) {
+  return (v << s) | (v >> (64 - s));
+}
+
+// ANS symbol(s) of one word, FloatTypeInfo<FT>::split
+// (float/GpuFloatUtils.cuh:190-370)
+template <int FT>
+__device__ __forceinline__ uint32_t compOf(typename FloatTraits<FT>::WordT w, int seg) {
+  if constexpr (FT == 0) {
+    return w;
+  } else if constexpr (FT == 1) {
+    return uint32_t(w) >> 8;
+  } else if constexpr (FT == 2) {
+    return (uint32_t(w) >> 7) & 0xffu;
+  } else if constexpr (FT == 3) {
+    return rotl32(w, 1) >> 24;
+  } else {
+    const uint64_t v = rotl64(w, 1);
+    return seg == 0 ? uint32_t(v >> 56) : uint32_t(v >> 48) & 0xffu;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// reductions / scans for NT-thread workgroups (NT multiple of 64)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t waveSum(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+__device__ __forceinline__ uint32_t waveXor(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v ^= __shfl_xor(v, o);
+  return v;
+}
+__device__ __forceinline__ uint32_t waveInclusiveScan(uint32_t v) {
+  const uint32_t lane = threadIdx.x & 63;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t u = __shfl_up(v, o);
+    if (lane >= uint32_t(o)) v += u;
+  }
+  return v;
+}
+template <int NT>
+__device__ __forceinline__ uint32_t blockSum(uint32_t v, uint32_t* smem) {
+  constexpr int W = NT / 64;
+  v = waveSum(v);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) smem[threadIdx.x >> 6] = v;
+  __syncthreads();
+  uint32_t t = 0;
+#pragma unroll
+  for (int i = 0; i < W; ++i) t += smem[i];
+  return t;
+}
+template <int NT>
+__device__ __forceinline__ uint32_t blockExclusiveScan(uint32_t v, uint32_t* smem,
+                                                       uint32_t* total) {
+  constexpr int W = NT / 64;
+  const uint32_t inc = waveInclusiveScan(v);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 63) smem[threadIdx.x >> 6] = inc;
+  __syncthreads();
+  uint32_t before = 0, all = 0;
+#pragma unroll
+  for (int i = 0; i < W; ++i) {
+    const uint32_t s = smem[i];
+    before += (i < int(threadIdx.x >> 6)) ? s : 0u;
+    all += s;
+  }
+  if (total) *total = all;
+  return before + inc - v;
+}
+
+// rANS decode table in LDS: LUT[s] = (s - cdf[sym]) << 20 | pdf << 8 | sym
+// (packDecodeLookup, ans/GpuANSDecode.cuh:34-44), built by an NT-thread
+// workgroup from the archive's u16 pdf table.
+template <int NT>
+__device__ __forceinline__ void buildLut(gp<const uint16_t> pdfIn, uint32_t* lut, uint32_t* red,
+                                         uint32_t* cdfS, uint32_t* pdfS) {
+  constexpr int kPer = kNumSymbols / NT;  // symbols per thread
+  const uint32_t tid = threadIdx.x;
+  uint32_t p[kPer], sum = 0;
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    p[k] = pdfIn[tid * kPer + k];
+    sum += p[k];
+  }
+  uint32_t c = blockExclusiveScan<NT>(sum, red, nullptr);
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    pdfS[tid * kPer + k] = p[k];
+    cdfS[tid * kPer + k] = c;
+    c += p[k];
+  }
+  __syncthreads();
+  const uint32_t lane = tid & 63;
+  for (uint32_t s = tid >> 6; s < kNumSymbols; s += NT / 64) {
+    const uint32_t ps = pdfS[s], cs = cdfS[s];
+    for (uint32_t j = lane; j < ps; j += 64) lut[cs + j] = (j << 20) | (ps << 8) | s;
+  }
+}
+
+}  // namespace dietgpu

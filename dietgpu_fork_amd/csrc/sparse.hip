@@ -20,7 +20,8 @@
 #include "codec_internal.h"
 #include "common.h"
 #include "dietgpu/GpuFloatCodec.h"
-#include "kernels.h"
+#include "decode.h"
+#include "encode.h"
 #include "profile.h"
 
 namespace dietgpu {
@@ -80,7 +81,7 @@ __global__ __launch_bounds__(kThreads) void k_sparseBitmap(BatchDesc in, const u
       }
     }
   }
-  cnt = blockSum(lane == 0 ? cnt : 0u, red);
+  cnt = blockSum<kThreads>(lane == 0 ? cnt : 0u, red);
   if (threadIdx.x == 0) tileCounts[uint64_t(b) * tilesPerElem + tile] = cnt;
 }
 
@@ -102,7 +103,7 @@ __global__ __launch_bounds__(kThreads) void k_sparseScan(BatchDesc in, uint32_t 
     const uint32_t t = t0 + threadIdx.x;
     const uint32_t v = t < tiles ? tc[t] : 0u;
     uint32_t total = 0;
-    const uint32_t ex = blockExclusiveScan(v, red, &total);
+    const uint32_t ex = blockExclusiveScan<kThreads>(v, red, &total);
     if (t < tiles) tc[t] = carry + ex;
     carry += total;
     __syncthreads();
@@ -195,7 +196,7 @@ __global__ __launch_bounds__(kThreads) void k_sparseHeaders(BatchDesc in, uint32
   for (uint32_t k = threadIdx.x; k < kTileWords / 8; k += kThreads) {
     if (bytes0 + k < bmBytes) c += __popc(a[16 + bytes0 + k]);
   }
-  c = blockSum(c, red);
+  c = blockSum<kThreads>(c, red);
   if (threadIdx.x == 0) tileCounts[uint64_t(b) * tilesPerElem + tile] = c;
 }
 
