@@ -126,7 +126,8 @@ void decodeBatchDevice(StackDeviceMemory& res, int pb, uint32_t nb, const BatchD
     const uint32_t ny = std::min(kMaxGridY, nb - y0);
     prof::Scope p("decode", s);
     dim3 g(std::max(1u, divUp(maxBlocks, DecCfg<FT>::kBlocksPerWG)), ny);
-    k_decode<FT><<<g, dec::kThreads, 0, s>>>(in, out, y0, pb, outSuccess_dev, outSize_dev);
+    k_decode<FT><<<g, dec::kThreads, DecCfg<FT>::ldsBytes(pb), s>>>(in, out, y0, pb,
+                                                                    outSuccess_dev, outSize_dev);
     HIP_LAUNCH_CHECK();
   }
 }

@@ -5,33 +5,36 @@
 // float/GpuFloatDecompress.cuh:39-841) in one pass, fp64 included.
 //
 // MI355X design:
-//  * 128-thread workgroups (2 waves).  A wave decodes K block *pairs*: lanes
-//    0-31 one block, lanes 32-63 the next (the reference's 32-state
-//    interleaving).  K = 2 independent pairs (fp64: one pair with two
-//    streams) give every step two independent state chains, and the step
-//    body is branch-free so hipcc interleaves them.
-//  * Per-half block bookkeeping (read pointer, ring window, data pointer)
-//    is wave-uniform and lives in SGPRs; per step the VALU does only the
-//    table lookup, state update, one v_mbcnt pair and the LDS word read.
-//  * The compressed words of each block are staged in an LDS ring (1024 u16
-//    per block, refilled 512 words at a time with one 16 B load per lane), so
-//    the reference's dependent read in[-prefix] is an LDS read.
-//  * Decoded symbols of a 1024-symbol segment go to LDS (1 byte / step); the
-//    segment is then joined with the raw float bytes (prefetched 16 B loads)
-//    and written with 16 B stores.
+//  * 256-thread workgroups (4 waves), 4 waves / SIMD.  A wave decodes K block
+//    *pairs*: lanes 0-31 one block, lanes 32-63 the next (the reference's
+//    32-state interleaving).  K = 2 independent pairs (fp64: one pair with
+//    two streams) give every step two independent state chains; the step is
+//    branch-free so they interleave.
+//  * 64-bit decode table {pdf | sym << 24, slot - cdf}: the state update is
+//    one v_mad_u32_u24 (u24 ignores the symbol byte), and `entry >> 16` =
+//    sym << 8 is stored with ds_write_b16_d16_hi -- already the high byte of
+//    an fp16 / bf16 word.  ds_read_b64 costs the same LDS cycles as b32.
+//  * Per-half block bookkeeping (read pointer, ring window, data pointer) is
+//    wave-uniform (SGPRs).  Compressed words are staged in a 512-word LDS
+//    ring per block stream; the next 256-word refill is prefetched into
+//    registers as soon as the previous one lands, so refills rarely wait on
+//    HBM.
+//  * 16-step segments are fully unrolled (constant LDS offsets); the
+//    decoded 512-word segment is joined with its raw float bytes (16 B loads
+//    issued before the segment) and written with 16 B stores.
 #pragma once
 
 #include "device.h"
 
 namespace dietgpu {
 namespace dec {
-constexpr int kThreads = 128;
+constexpr int kThreads = 256;
 constexpr int kWaves = kThreads / 64;
-constexpr uint32_t kRing = 1024;    // u16 words per block ring
-constexpr uint32_t kRefill = 512;   // words per refill (64 lanes x 16 B)
-constexpr uint32_t kSegSteps = 32;  // decode steps per output segment
+constexpr uint32_t kRing = 512;      // u16 words per block-stream ring
+constexpr uint32_t kRefill = 256;    // words per refill (64 lanes x 8 B)
+constexpr uint32_t kSegSteps = 16;   // decode steps per output segment
 constexpr uint32_t kSegWords = kSegSteps * 32;
-constexpr uint32_t kUnroll = 4;     // steps between ring checks
+constexpr uint32_t kUnroll = 4;      // steps between ring checks
 }  // namespace dec
 
 #define DG_L __attribute__((address_space(3)))
@@ -44,69 +47,77 @@ struct DecCfg {
   static constexpr int K = S == 2 ? 1 : 2;          // block pairs per wave
   static constexpr int kBlocksPerWave = 2 * K;
   static constexpr int kBlocksPerWG = dec::kWaves * kBlocksPerWave;
-  // 16-byte raw vectors per 16-word chunk
-  static constexpr int kRawVecs = FT == 0 ? 0 : (FT <= 2 ? 1 : (FT == 3 ? 3 : 6));
+  static constexpr uint32_t kHalfStreams = dec::kWaves * K * S * 2;
+  static constexpr uint32_t kRingBytes = kHalfStreams * dec::kRing * 2;
+  static constexpr uint32_t kSegBytes = kHalfStreams * dec::kSegWords * 2;
+  // dynamic LDS: S tables of 8 << pb bytes, rings, segment buffers
+  __host__ __device__ static constexpr uint32_t lutBytes(int pb) { return S * (8u << pb); }
+  __host__ __device__ static constexpr uint32_t ldsBytes(int pb) {
+    return lutBytes(pb) + kRingBytes + kSegBytes;
+  }
 };
 
-// One stream of one block pair.  Everything but x / ringLane is wave-uniform.
-struct DPair {
+// One ANS stream of one block pair.  All but x / pf are wave-uniform.
+struct DStream {
   uint32_t x;                   // this lane's rANS state
+  lp<uint16_t> ring;            // LDS ring of half 0 (half 1 follows)
   lp<const uint16_t> ringLane;  // this lane's half ring
   int32_t ptr[2];               // per half: next read is below ptr
   int32_t lo[2];                // per half: ring holds stream words >= lo
   gp<const uint16_t> data[2];   // per half: block's compressed words (HBM)
-  lp<uint16_t> ring[2];         // per half: LDS ring
+  u32x2 pf[2];                  // per half: prefetched words [lo - 256, lo)
 };
 
-// Copy stream words [a, b) (a multiple of 8, b - a <= 512) of one half into
-// its ring with the whole wave (one 16 B load per lane).  May read up to 7
-// words past b: the block padding every archive has.
-__device__ __forceinline__ void ringFill(gp<const uint16_t> data, lp<uint16_t> ring, int32_t a,
-                                         int32_t b, uint32_t lane, bool vec) {
-  if (vec) {
-    const int32_t j = int32_t(lane);
-    if (j < ((b - a + 7) >> 3)) {
-      const uint4 v = ld16((gp<const uint4>)(data + a) + j);
-      *(lp<u32x4>)(ring + ((a + 8 * j) & int32_t(dec::kRing - 1))) = u32x4{v.x, v.y, v.z, v.w};
-    }
-  } else {
-    for (int32_t k = a + int32_t(lane); k < b; k += 64) ring[k & int32_t(dec::kRing - 1)] = data[k];
-  }
+// 4 compressed words at p (8 B load when aligned)
+__device__ __forceinline__ u32x2 ld4w(gp<const uint16_t> p, bool vec) {
+  if (vec) return *(gp<const u32x2>)p;
+  return u32x2{uint32_t(p[0]) | (uint32_t(p[1]) << 16), uint32_t(p[2]) | (uint32_t(p[3]) << 16)};
 }
 
-// Ensure the next kUnroll steps of both halves find their words in the ring.
-__device__ __forceinline__ void ringEnsure(DPair& p, uint32_t lane, bool vec) {
+// Prefetch words [max(0, lo - 256), lo) of one half (lane j: 4 words).
+// May read up to 3 words past lo: inside the block's 8-word padding.
+__device__ __forceinline__ void ringPrefetch(DStream& p, int hh, uint32_t lane, bool vec) {
+  const int32_t nlo = max(0, p.lo[hh] - int32_t(dec::kRefill));
+  if (p.lo[hh] > 0 && int32_t(4 * lane) < p.lo[hh] - nlo)
+    p.pf[hh] = ld4w(p.data[hh] + nlo + 4 * lane, vec);
+}
+
+// Keep the next kUnroll steps' words of both halves in the ring.
+__device__ __forceinline__ void ringEnsure(DStream& p, uint32_t lane, bool vec) {
 #pragma unroll
   for (int hh = 0; hh < 2; ++hh) {
     if (p.lo[hh] > 0 && p.ptr[hh] - int32_t(32 * dec::kUnroll) < p.lo[hh]) {
+      // the refill overwrites words >= lo + 256, all consumed (ptr < lo + 128)
       const int32_t nlo = max(0, p.lo[hh] - int32_t(dec::kRefill));
-      ringFill(p.data[hh], p.ring[hh], nlo, p.lo[hh], lane, vec);
+      if (int32_t(4 * lane) < p.lo[hh] - nlo)
+        *(lp<u32x2>)(p.ring + hh * dec::kRing + ((nlo + 4 * lane) & (dec::kRing - 1))) = p.pf[hh];
       p.lo[hh] = nlo;
+      ringPrefetch(p, hh, lane, vec);
     }
   }
 }
 
 // One LIFO decode step (decodeOneWarp, ans/GpuANSDecode.cuh:55-105) of one
-// stream of a block pair.  hv: all-ones on lanes 32-63.  Returns the LUT
-// entry (symbol in bits 0-7).  kMask: lanes with !valid keep their state and
-// do not read.
+// stream of a block pair.  hv: all-ones on lanes 32-63 (opaque to the
+// compiler).  Returns the table entry's low word (sym in bits 24-31).
+// kMask: lanes with !valid keep their state and do not read.
 template <bool kMask>
-__device__ __forceinline__ uint32_t decStep(DPair& p, bool valid, lp<const uint32_t> lut,
+__device__ __forceinline__ uint32_t decStep(DStream& p, bool valid, lp<const u32x2> lut,
                                             uint32_t mask, int pb, uint32_t hv) {
-  const uint32_t e = lut[p.x & mask];
-  uint32_t xn = __umul24((e >> 8) & 0xfffu, p.x >> pb) + (e >> 20);
+  const u32x2 e = lut[p.x & mask];
+  uint32_t xn = __umul24(e.x, p.x >> pb) + e.y;
   if (kMask) xn = valid ? xn : p.x;
   const bool rd = kMask ? (valid && xn < kMinState) : (xn < kMinState);
   const uint64_t vote = ballot(rd);
   const int32_t cLo = __popc(uint32_t(vote));
   const int32_t cHi = __popc(uint32_t(vote >> 32));
-  // read index = ptr' + (#readers of my half below me); mbcnt over 64 lanes
-  // already counts all low-half readers for lanes 32-63.
+  // read index = ptr' + (#readers of my half below me); v_mbcnt over 64
+  // lanes already counts every low-half reader for lanes 32-63.
   const int32_t baseLo = p.ptr[0] - cLo;
-  const int32_t baseHi = p.ptr[1] - cHi - cLo;
+  const int32_t diff = p.ptr[1] - p.ptr[0] - cHi;  // (ptr1 - cHi - cLo) - baseLo
   p.ptr[0] = baseLo;
   p.ptr[1] -= cHi;
-  const uint32_t vbase = uint32_t(baseLo) + (hv & uint32_t(baseHi - baseLo));
+  const uint32_t vbase = uint32_t(baseLo) + (hv & uint32_t(diff));
   const uint32_t idx = __builtin_amdgcn_mbcnt_hi(uint32_t(vote >> 32),
                                                  __builtin_amdgcn_mbcnt_lo(uint32_t(vote), vbase));
   const uint32_t v = p.ringLane[idx & (dec::kRing - 1)];  // harmless for non-readers
@@ -114,17 +125,16 @@ __device__ __forceinline__ uint32_t decStep(DPair& p, bool valid, lp<const uint3
   // intrinsic (not a select) keeps the LDS read unconditional: a branch
   // around it would split the step and serialise the independent chains.
   p.x = __builtin_amdgcn_perm(xn, v, rd ? 0x05040100u : 0x07060504u);
-  return e;
+  return e.x;
 }
 
-// Join 16 decoded symbols (LDS) with their raw bytes into output words.
+// Join 16 decoded symbols (u16 sym << 8 in LDS) with their raw bytes.
 template <int FT>
 struct Join {
   using WordT = typename FloatTraits<FT>::WordT;
-  static constexpr int kRawVecs = DecCfg<FT>::kRawVecs;
-  static constexpr int kR = kRawVecs > 0 ? kRawVecs : 1;
+  static constexpr int kR = FT == 0 ? 1 : (FT <= 2 ? 1 : (FT == 3 ? 3 : 6));
 
-  // prefetch the raw vectors of the chunk starting at word i0
+  // raw vectors of the chunk starting at word i0 (16 B loads)
   static __device__ __forceinline__ void load(uint4 (&r)[kR], gp<const uint8_t> raw, uint32_t n,
                                               uint32_t i0) {
     if constexpr (FT == 1 || FT == 2) {
@@ -142,6 +152,7 @@ struct Join {
     }
   }
 
+  // scalar join of word i (s0, s1: symbols)
   static __device__ __forceinline__ WordT one(uint32_t s0, uint32_t s1, gp<const uint8_t> raw,
                                               uint32_t n, uint32_t i) {
     if constexpr (FT == 0) {
@@ -163,76 +174,92 @@ struct Join {
     }
   }
 
-  // vector join of a full chunk: out[i0 .. i0+16)
-  static __device__ __forceinline__ void vec(gp<uint8_t> outB, uint32_t i0, uint4 sv, uint4 sv1,
-                                             const uint4 (&r)[kR]) {
-    const uint32_t sw[4] = {sv.x, sv.y, sv.z, sv.w};
+  // [raw_a, sym0, raw_b, sym1] from a symbol pair (syms at bytes 1, 3) and
+  // raw bytes a, b = bytes 2*odd, 2*odd + 1 of rw
+  static __device__ __forceinline__ uint32_t pair16(uint32_t sp, uint32_t rw, int odd) {
+    return __builtin_amdgcn_perm(sp, rw, odd ? 0x07030502u : 0x07010500u);
+  }
+
+  // vector join of a full chunk: out words [i0, i0 + 16).  s / s1: 8 dwords
+  // of u16 (sym << 8) of stream 0 / 1.
+  static __device__ __forceinline__ void vec(gp<uint8_t> outB, uint32_t i0, const uint32_t (&s)[8],
+                                             const uint32_t (&s1)[8], const uint4 (&r)[kR]) {
     if constexpr (FT == 0) {
-      st16(outB + i0, sv);
+      uint32_t o[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) o[k] = __builtin_amdgcn_perm(s[2 * k + 1], s[2 * k], 0x07050301u);
+      st16(outB + i0, make_uint4(o[0], o[1], o[2], o[3]));
     } else if constexpr (FT == 1 || FT == 2) {
       const uint32_t rw[4] = {r[0].x, r[0].y, r[0].z, r[0].w};
       uint32_t o[8];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        // words 4k..4k+3: bytes of sw[k] / rw[k] spread into 16-bit lanes
-        const uint32_t s01 = __builtin_amdgcn_perm(0u, sw[k], 0x0c010c00u);
-        const uint32_t s23 = __builtin_amdgcn_perm(0u, sw[k], 0x0c030c02u);
-        const uint32_t r01 = __builtin_amdgcn_perm(0u, rw[k], 0x0c010c00u);
-        const uint32_t r23 = __builtin_amdgcn_perm(0u, rw[k], 0x0c030c02u);
-        if constexpr (FT == 1) {
-          o[2 * k] = (s01 << 8) | r01;
-          o[2 * k + 1] = (s23 << 8) | r23;
-        } else {
-          o[2 * k] = (s01 << 7) | ((r01 >> 1) & 0x007f007fu) | ((r01 & 0x00010001u) << 15);
-          o[2 * k + 1] = (s23 << 7) | ((r23 >> 1) & 0x007f007fu) | ((r23 & 0x00010001u) << 15);
-        }
+      for (int k = 0; k < 8; ++k) {
+        const uint32_t t = pair16(s[k], rw[k >> 1], k & 1);  // exp << 8 | raw per half
+        // bf16: rotate each 16-bit half right by one (raw = mant << 1 | sign)
+        o[k] = FT == 1 ? t : (((t >> 1) & 0x7fff7fffu) | ((t << 15) & 0x80008000u));
       }
       gp<uint4> d = (gp<uint4>)(outB + 2 * i0);
       st16(d, make_uint4(o[0], o[1], o[2], o[3]));
       st16(d + 1, make_uint4(o[4], o[5], o[6], o[7]));
     } else if constexpr (FT == 3) {
-      const uint32_t lo[8] = {r[0].x, r[0].y, r[0].z, r[0].w, r[1].x, r[1].y, r[1].z, r[1].w};
-      const uint32_t hb[4] = {r[2].x, r[2].y, r[2].z, r[2].w};
+      const uint32_t lw[8] = {r[0].x, r[0].y, r[0].z, r[0].w, r[1].x, r[1].y, r[1].z, r[1].w};
+      const uint32_t hw[4] = {r[2].x, r[2].y, r[2].z, r[2].w};
       uint32_t o[16];
 #pragma unroll
-      for (int k = 0; k < 16; ++k) {
-        const uint32_t s = (sw[k >> 2] >> (8 * (k & 3))) & 0xffu;
-        const uint32_t h8 = (hb[k >> 2] >> (8 * (k & 3))) & 0xffu;
-        const uint32_t l16 = (lo[k >> 1] >> (16 * (k & 1))) & 0xffffu;
-        o[k] = rotr32((s << 24) | (h8 << 16) | l16, 1);
+      for (int k = 0; k < 8; ++k) {
+        const uint32_t h = pair16(s[k], hw[k >> 1], k & 1);  // [hb, sym] x 2
+        const uint32_t w0 = __builtin_amdgcn_perm(h, lw[k], 0x05040100u);
+        const uint32_t w1 = __builtin_amdgcn_perm(h, lw[k], 0x07060302u);
+        o[2 * k] = __builtin_amdgcn_alignbit(w0, w0, 1);
+        o[2 * k + 1] = __builtin_amdgcn_alignbit(w1, w1, 1);
       }
       gp<uint4> d = (gp<uint4>)(outB + 4 * i0);
 #pragma unroll
       for (int k = 0; k < 4; ++k) st16(d + k, make_uint4(o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]));
     } else {
-      const uint32_t sw1[4] = {sv1.x, sv1.y, sv1.z, sv1.w};
-      const uint32_t lo[16] = {r[0].x, r[0].y, r[0].z, r[0].w, r[1].x, r[1].y, r[1].z, r[1].w,
+      const uint32_t lw[16] = {r[0].x, r[0].y, r[0].z, r[0].w, r[1].x, r[1].y, r[1].z, r[1].w,
                                r[2].x, r[2].y, r[2].z, r[2].w, r[3].x, r[3].y, r[3].z, r[3].w};
       const uint32_t hw[8] = {r[4].x, r[4].y, r[4].z, r[4].w, r[5].x, r[5].y, r[5].z, r[5].w};
       gp<uint4> d = (gp<uint4>)(outB + 8 * i0);
 #pragma unroll
-      for (int k = 0; k < 16; k += 2) {
-        uint32_t o[4];
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-          const int kk = k + q;
-          const uint32_t s0 = (sw[kk >> 2] >> (8 * (kk & 3))) & 0xffu;
-          const uint32_t s1 = (sw1[kk >> 2] >> (8 * (kk & 3))) & 0xffu;
-          const uint32_t h16 = (hw[kk >> 1] >> (16 * (kk & 1))) & 0xffffu;
-          // v = s0:s1:h16:lo (64 bits); w = rotr64(v, 1)
-          const uint32_t vhi = (s0 << 24) | (s1 << 16) | h16;
-          const uint32_t vlo = lo[kk];
-          o[2 * q] = (vlo >> 1) | (vhi << 31);
-          o[2 * q + 1] = (vhi >> 1) | (vlo << 31);
-        }
-        st16(d + (k >> 1), make_uint4(o[0], o[1], o[2], o[3]));
+      for (int k = 0; k < 8; ++k) {
+        // [s1, s0] pairs, then vhi = [h16, s1, s0] per word; w = rotr64(vhi:lo, 1)
+        const uint32_t p = __builtin_amdgcn_perm(s[k], s1[k], 0x07030501u);
+        const uint32_t vh0 = __builtin_amdgcn_perm(p, hw[k], 0x05040100u);
+        const uint32_t vh1 = __builtin_amdgcn_perm(p, hw[k], 0x07060302u);
+        const uint32_t l0 = lw[2 * k], l1 = lw[2 * k + 1];
+        st16(d + k, make_uint4(__builtin_amdgcn_alignbit(vh0, l0, 1), __builtin_amdgcn_alignbit(l0, vh0, 1),
+                               __builtin_amdgcn_alignbit(vh1, l1, 1), __builtin_amdgcn_alignbit(l1, vh1, 1)));
       }
     }
   }
 };
 
-// grid (ceil(maxBlocks / kBlocksPerWG), batch).  out.size(b) = capacity
-// (bytes for raw ANS, words for floats).
+// 64-bit decode table of one archive: entry[slot] = {pdf | sym << 24,
+// slot - cdf[sym]} (packDecodeLookup, ans/GpuANSDecode.cuh:34-44, re-laid
+// out for v_mad_u32_u24).  scratch: >= 2 * 256 + 4 dwords of LDS.
+__device__ __forceinline__ void buildLut64(gp<const uint16_t> pdfIn, lp<u32x2> lut,
+                                           uint32_t* scratch) {
+  static_assert(dec::kThreads == kNumSymbols, "one symbol per thread");
+  uint32_t* cdfS = scratch;
+  uint32_t* pdfS = scratch + kNumSymbols;
+  uint32_t* red = scratch + 2 * kNumSymbols;
+  const uint32_t tid = threadIdx.x;
+  const uint32_t p = pdfIn[tid];
+  const uint32_t c = blockExclusiveScan<dec::kThreads>(p, red, nullptr);
+  pdfS[tid] = p;
+  cdfS[tid] = c;
+  __syncthreads();
+  const uint32_t lane = tid & 63;
+  for (uint32_t s = tid >> 6; s < kNumSymbols; s += dec::kWaves) {
+    const uint32_t ps = pdfS[s], cs = cdfS[s];
+    for (uint32_t j = lane; j < ps; j += 64) lut[cs + j] = u32x2{ps | (s << 24), j};
+  }
+}
+
+// grid (ceil(maxBlocks / kBlocksPerWG), batch), dynamic LDS
+// DecCfg<FT>::ldsBytes(pb).  out.size(b) = capacity (bytes for raw ANS,
+// words for floats).
 template <int FT>
 __global__ __launch_bounds__(dec::kThreads) void k_decode(BatchDesc in, BatchDesc out,
                                                           uint32_t batchOffset, int pb,
@@ -241,12 +268,11 @@ __global__ __launch_bounds__(dec::kThreads) void k_decode(BatchDesc in, BatchDes
   using Cfg = DecCfg<FT>;
   using WordT = typename FloatTraits<FT>::WordT;
   constexpr int S = Cfg::S, K = Cfg::K, R = Join<FT>::kR;
-  __shared__ uint32_t lutS[S][1u << 11];
-  __shared__ __attribute__((aligned(16))) uint16_t ringS[dec::kWaves][K][S][2][dec::kRing];
-  __shared__ __attribute__((aligned(16))) uint8_t segS[dec::kWaves][K][S][2][dec::kSegWords];
-  __shared__ uint32_t red[dec::kWaves];
-  __shared__ uint32_t cdfS[kNumSymbols];
-  __shared__ uint32_t pdfS[kNumSymbols];
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  lp<uint8_t> L = (lp<uint8_t>)smem;
+  const uint32_t lutBytes = Cfg::lutBytes(pb);
+  lp<uint16_t> ringAll = (lp<uint16_t>)(L + lutBytes);
+  lp<uint16_t> segAll = (lp<uint16_t>)(L + lutBytes + Cfg::kRingBytes);
 
   const uint32_t b = batchOffset + blockIdx.y;
   const uint32_t tid = threadIdx.x;
@@ -281,13 +307,14 @@ __global__ __launch_bounds__(dec::kThreads) void k_decode(BatchDesc in, BatchDes
 
 #pragma unroll
   for (int s = 0; s < S; ++s) {
-    buildLut<dec::kThreads>((gp<const uint16_t>)(arch[s] + kANSHeaderBytes), lutS[s], red, cdfS,
-                            pdfS);
+    buildLut64((gp<const uint16_t>)(arch[s] + kANSHeaderBytes),
+               (lp<u32x2>)(L + s * (lutBytes / S)), (uint32_t*)segAll);
     __syncthreads();
   }
 
   const uint32_t w = readfirst(tid >> 6), lane = tid & 63, l = lane & 31;
-  const uint32_t hv = lane >= 32 ? ~0u : 0u;
+  uint32_t hv = lane >= 32 ? ~0u : 0u;
+  asm volatile("" : "+v"(hv));  // keep `hv & x` a v_and (not a v_cndmask pair)
   const uint32_t blk0 = blockIdx.x * Cfg::kBlocksPerWG + w * Cfg::kBlocksPerWave;
   if (blk0 >= nBlocks) return;
 
@@ -299,7 +326,8 @@ __global__ __launch_bounds__(dec::kThreads) void k_decode(BatchDesc in, BatchDes
 
   // per pair c: blocks blk0 + 2c (lanes 0-31) and blk0 + 2c + 1 (lanes 32-63)
   uint32_t uwH[K][2];  // wave-uniform
-  DPair st[K][S];
+  DStream st[K][S];
+  lp<uint16_t> segLane[K][S];
 #pragma unroll
   for (int c = 0; c < K; ++c) {
 #pragma unroll
@@ -307,31 +335,37 @@ __global__ __launch_bounds__(dec::kThreads) void k_decode(BatchDesc in, BatchDes
       gp<const uint8_t> states = arch[s] + kANSHeaderBytes + kPdfBytes;
       gp<const uint2> bw = (gp<const uint2>)(states + uint64_t(kStateBytesPerBlock) * nBlocks);
       gp<const uint16_t> data = (gp<const uint16_t>)(bw + roundUp(nBlocks, 2));
-      DPair& d = st[c][s];
+      DStream& d = st[c][s];
+      const uint32_t hs = (w * K + c) * S + s;  // half-stream pair index
+      d.ring = ringAll + hs * 2 * dec::kRing;
+      d.ringLane = d.ring + (hv & dec::kRing);
+      segLane[c][s] = segAll + hs * 2 * dec::kSegWords + (hv & dec::kSegWords) + l;
 #pragma unroll
       for (int hh = 0; hh < 2; ++hh) {
         const uint32_t bk = blk0 + 2 * c + hh;
-        d.ring[hh] = (lp<uint16_t>)&ringS[w][c][s][hh][0];
+        uwH[c][hh] = 0;
+        d.ptr[hh] = 0;
+        d.lo[hh] = 0;
+        d.data[hh] = data;
+        d.pf[hh] = u32x2{0, 0};
         if (bk < nBlocks) {
           const uint2 e = ld8(bw + bk);
           uwH[c][hh] = e.x >> 16;
-          d.ptr[hh] = int32_t(e.x & 0xffffu);
+          const int32_t cw = int32_t(e.x & 0xffffu);
+          d.ptr[hh] = cw;
           d.data[hh] = data + e.y;
-          d.lo[hh] = d.ptr[hh] > int32_t(dec::kRing)
-                         ? int32_t(roundUp(uint32_t(d.ptr[hh]) - dec::kRing, 8))
-                         : 0;
-          // initial fill of [lo, cw) (<= 1024 words: two wave-wide passes)
-          ringFill(d.data[hh], d.ring[hh], d.lo[hh], min(d.ptr[hh], d.lo[hh] + 512), lane, vecIn);
-          if (d.ptr[hh] > d.lo[hh] + 512)
-            ringFill(d.data[hh], d.ring[hh], d.lo[hh] + 512, d.ptr[hh], lane, vecIn);
-        } else {
-          uwH[c][hh] = 0;
-          d.ptr[hh] = 0;
-          d.lo[hh] = 0;
-          d.data[hh] = data;
+          const int32_t lo = cw > int32_t(dec::kRing) ? int32_t(roundUp(uint32_t(cw) - dec::kRing, 4)) : 0;
+          d.lo[hh] = lo;
+          // initial fill of [lo, cw) (<= 512 words: two wave-wide passes)
+#pragma unroll
+          for (int q = 0; q < 2; ++q) {
+            const int32_t a = lo + q * int32_t(dec::kRefill) + int32_t(4 * lane);
+            if (a < cw)
+              *(lp<u32x2>)(d.ring + hh * dec::kRing + (a & (dec::kRing - 1))) = ld4w(d.data[hh] + a, vecIn);
+          }
+          ringPrefetch(d, hh, lane, vecIn);
         }
       }
-      d.ringLane = lane >= 32 ? (lp<const uint16_t>)d.ring[1] : (lp<const uint16_t>)d.ring[0];
       const uint32_t bkMine = blk0 + 2 * c + (lane >> 5);
       d.x = bkMine < nBlocks
                 ? ((gp<const uint32_t>)(states + uint64_t(kStateBytesPerBlock) * bkMine))[l]
@@ -343,19 +377,21 @@ __global__ __launch_bounds__(dec::kThreads) void k_decode(BatchDesc in, BatchDes
 #pragma unroll
   for (int c = 0; c < K; ++c) T = max(T, max(divUp(uwH[c][0], 32), divUp(uwH[c][1], 32)));
 
+  lp<const u32x2> lut[S];
+#pragma unroll
+  for (int s = 0; s < S; ++s) lut[s] = (lp<const u32x2>)(L + s * (lutBytes / S));
+
   for (int32_t g = int32_t(T - 1) / int32_t(dec::kSegSteps); g >= 0; --g) {
     const uint32_t segW0 = uint32_t(g) * dec::kSegWords;  // first word of segment in block
-    // prefetch the raw bytes of this segment's full chunks
-    uint4 rv[K][2][R];
+    const uint32_t off = 16 * l;                           // this lane's chunk in the segment
+    // prefetch the raw bytes of this segment's chunks
+    uint4 rv[K][R];
 #pragma unroll
     for (int c = 0; c < K; ++c) {
       const uint32_t uw = lane >= 32 ? uwH[c][1] : uwH[c][0];
       const uint32_t bk = blk0 + 2 * c + (lane >> 5);
-#pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        const uint32_t off = segW0 + 16 * (l + 32 * q);
-        if (FT != 0 && vecIn && off + 16 <= uw) Join<FT>::load(rv[c][q], raw, n, bk * kBlockSize + off);
-      }
+      if (FT != 0 && vecIn && segW0 + off + 16 <= uw)
+        Join<FT>::load(rv[c], raw, n, bk * kBlockSize + segW0 + off);
     }
 
     bool full = true;
@@ -363,73 +399,78 @@ __global__ __launch_bounds__(dec::kThreads) void k_decode(BatchDesc in, BatchDes
     for (int c = 0; c < K; ++c)
       full = full && uwH[c][0] >= segW0 + dec::kSegWords && uwH[c][1] >= segW0 + dec::kSegWords;
 
-    const int32_t tTop = min(int32_t(T) - 1, g * int32_t(dec::kSegSteps) + int32_t(dec::kSegSteps) - 1);
-    const int32_t tBot = g * int32_t(dec::kSegSteps);
     if (full) {
-      for (int32_t t0 = tTop; t0 >= tBot; t0 -= int32_t(dec::kUnroll)) {
+#pragma unroll
+      for (int grp = int(dec::kSegSteps / dec::kUnroll) - 1; grp >= 0; --grp) {
 #pragma unroll
         for (int c = 0; c < K; ++c)
 #pragma unroll
           for (int s = 0; s < S; ++s) ringEnsure(st[c][s], lane, vecIn);
 #pragma unroll
-        for (uint32_t u = 0; u < dec::kUnroll; ++u) {
-          const uint32_t si = uint32_t(t0 - int32_t(u) - tBot) * 32 + l;
+        for (int u = int(dec::kUnroll) - 1; u >= 0; --u) {
+          const int tr = grp * int(dec::kUnroll) + u;  // step within segment
 #pragma unroll
           for (int c = 0; c < K; ++c)
 #pragma unroll
             for (int s = 0; s < S; ++s) {
-              const uint32_t e = decStep<false>(st[c][s], true, (lp<const uint32_t>)lutS[s], mask, pb, hv);
-              segS[w][c][s][lane >> 5][si] = uint8_t(e);
+              const uint32_t e = decStep<false>(st[c][s], true, lut[s], mask, pb, hv);
+              segLane[c][s][tr * 32] = uint16_t(e >> 16);
             }
         }
       }
     } else {
+      const int32_t tTop = min(int32_t(T) - 1, g * int32_t(dec::kSegSteps) + int32_t(dec::kSegSteps) - 1);
+      const int32_t tBot = g * int32_t(dec::kSegSteps);
       for (int32_t t = tTop; t >= tBot; --t) {
 #pragma unroll
         for (int c = 0; c < K; ++c)
 #pragma unroll
           for (int s = 0; s < S; ++s) ringEnsure(st[c][s], lane, vecIn);
-        const uint32_t si = uint32_t(t - tBot) * 32 + l;
 #pragma unroll
         for (int c = 0; c < K; ++c) {
           const uint32_t uw = lane >= 32 ? uwH[c][1] : uwH[c][0];
           const bool valid = uint32_t(t) * 32 + l < uw;
 #pragma unroll
           for (int s = 0; s < S; ++s) {
-            const uint32_t e = decStep<true>(st[c][s], valid, (lp<const uint32_t>)lutS[s], mask, pb, hv);
-            if (valid) segS[w][c][s][lane >> 5][si] = uint8_t(e);
+            const uint32_t e = decStep<true>(st[c][s], valid, lut[s], mask, pb, hv);
+            if (valid) segLane[c][s][(t - tBot) * 32] = uint16_t(e >> 16);
           }
         }
       }
     }
+    __builtin_amdgcn_wave_barrier();
 
     // join + store this segment
 #pragma unroll
     for (int c = 0; c < K; ++c) {
       const uint32_t uw = lane >= 32 ? uwH[c][1] : uwH[c][0];
       const uint32_t bk = blk0 + 2 * c + (lane >> 5);
-      if (uw <= segW0) continue;
-      const uint32_t segCnt = min(dec::kSegWords, uw - segW0);
-#pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        const uint32_t off = 16 * (l + 32 * q);  // word offset inside the segment
-        if (off >= segCnt) continue;
-        const uint32_t i0 = bk * kBlockSize + segW0 + off;
-        lp<const uint8_t> s0 = (lp<const uint8_t>)&segS[w][c][0][lane >> 5][off];
-        lp<const uint8_t> s1 = (lp<const uint8_t>)&segS[w][c][S - 1][lane >> 5][off];
-        if ((FT == 0 || vecIn) && vecOut && off + 16 <= segCnt) {
-          const u32x4 p0 = *(lp<const u32x4>)s0;
-          const u32x4 p1 = *(lp<const u32x4>)s1;
-          const uint4 a = make_uint4(p0.x, p0.y, p0.z, p0.w);
-          const uint4 a1 = make_uint4(p1.x, p1.y, p1.z, p1.w);
-          Join<FT>::vec(outB, i0, a, a1, rv[c][q]);
+      if (segW0 + off >= uw) continue;
+      const uint32_t cnt = min(16u, uw - segW0 - off);
+      const uint32_t i0 = bk * kBlockSize + segW0 + off;
+      lp<const uint16_t> q0 = segLane[c][0] - l + off;
+      lp<const uint16_t> q1 = segLane[c][S - 1] - l + off;
+      if ((FT == 0 || vecIn) && vecOut && cnt == 16) {
+        uint32_t sv[8], sv1[8];
+        const u32x4 a0 = *(lp<const u32x4>)q0, a1 = *(lp<const u32x4>)(q0 + 8);
+        sv[0] = a0.x; sv[1] = a0.y; sv[2] = a0.z; sv[3] = a0.w;
+        sv[4] = a1.x; sv[5] = a1.y; sv[6] = a1.z; sv[7] = a1.w;
+        if constexpr (S == 2) {
+          const u32x4 b0 = *(lp<const u32x4>)q1, b1 = *(lp<const u32x4>)(q1 + 8);
+          sv1[0] = b0.x; sv1[1] = b0.y; sv1[2] = b0.z; sv1[3] = b0.w;
+          sv1[4] = b1.x; sv1[5] = b1.y; sv1[6] = b1.z; sv1[7] = b1.w;
         } else {
-          const uint32_t cnt = min(16u, segCnt - off);
-          gp<WordT> o = (gp<WordT>)outB;
-          for (uint32_t k = 0; k < cnt; ++k) o[i0 + k] = Join<FT>::one(s0[k], s1[k], raw, n, i0 + k);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) sv1[k] = 0;
         }
+        Join<FT>::vec(outB, i0, sv, sv1, rv[c]);
+      } else {
+        gp<WordT> o = (gp<WordT>)outB;
+        for (uint32_t k = 0; k < cnt; ++k)
+          o[i0 + k] = Join<FT>::one(q0[k] >> 8, q1[k] >> 8, raw, n, i0 + k);
       }
     }
+    __builtin_amdgcn_wave_barrier();
   }
 }
 
