@@ -37,10 +37,6 @@ constexpr uint32_t kSegWords = kSegSteps * 32;
 constexpr uint32_t kUnroll = 4;      // steps between ring checks
 }  // namespace dec
 
-#define DG_L __attribute__((address_space(3)))
-template <typename T>
-using lp = DG_L T*;
-
 template <int FT>
 struct DecCfg {
   static constexpr int S = FloatTraits<FT>::kSegs;  // ANS streams per word

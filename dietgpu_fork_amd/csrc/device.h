@@ -13,6 +13,11 @@ namespace dietgpu {
 template <typename T>
 using gp = DG_G T*;
 
+// LDS pointers (address_space(3)): ds_* instructions with 32-bit addresses
+#define DG_L __attribute__((address_space(3)))
+template <typename T>
+using lp = DG_L T*;
+
 template <typename T>
 __device__ __forceinline__ gp<T> G(T* p) {
   return (gp<T>)p;

@@ -14,6 +14,8 @@
 //                   (float/GpuFloatCompress.cuh:557-667)
 #pragma once
 
+#include <type_traits>
+
 #include "device.h"
 
 namespace dietgpu {
@@ -194,19 +196,27 @@ static __global__ __launch_bounds__(kThreads) void k_normalize(
 
 // ---------------------------------------------------------------------------
 // k_encode: fused split + rANS encode.
-//   * 128-thread workgroups; a half-wave codes one 4 KiB block; each lane
-//     runs K blocks (K = 2, fp64: K = 1 with its two streams) for ILP.
-//   * Per 1024-symbol segment the wave loads the block's words with 16 B
-//     loads (issued one segment ahead), writes the float raw bytes straight
-//     into the archive's raw section and the ANS symbols into LDS, then runs
-//     32 encode steps per block from LDS.
-//   * Emitted u16 words go to a per-block scratch slot; k_coalesce packs the
+//   * 256-thread workgroups (4 waves).  Lanes 0-31 / 32-63 of a wave code
+//     one 4 KiB block each; each wave runs K block pairs (K = 2; fp64: K = 1
+//     with its two streams) as independent chains.
+//   * Per 512-symbol segment the wave splits 16 B input vectors (loaded one
+//     segment ahead): float raw bytes go straight to the archive's raw
+//     section, ANS symbols to LDS.  It then runs 16 branch-free encode steps
+//     per block from LDS (fully unrolled).
+//   * Emitted u16 words go to a 512-word LDS ring per block stream (writers
+//     at ascending lane order; non-writers store to a per-lane trash dword so
+//     the step has no branch); rings are flushed to the block's scratch slot
+//     256 words at a time with one 8 B store per lane.  k_coalesce packs the
 //     slots into the archive.
 // ---------------------------------------------------------------------------
 namespace enc {
-constexpr int kThreads = 128;
+constexpr int kThreads = 256;
 constexpr int kWaves = kThreads / 64;
-constexpr uint32_t kSegWords = 1024;
+constexpr uint32_t kSegSteps = 16;
+constexpr uint32_t kSegWords = kSegSteps * 32;
+constexpr uint32_t kRing = 512;    // u16 words per block-stream output ring
+constexpr uint32_t kFlush = 256;   // words per flush (64 lanes x 8 B)
+constexpr uint32_t kUnroll = 4;    // steps between flush checks
 }  // namespace enc
 
 template <int FT>
@@ -217,85 +227,125 @@ struct EncCfg {
   static constexpr int kBlocksPerWave = 2 * K;
   static constexpr int kBlocksPerWG = enc::kWaves * kBlocksPerWave;
   // 16-byte input vectors per lane per block per segment (32 lanes x V x 16 B
-  // = 1024 words)
+  // = 512 words)
   static constexpr int V = int(enc::kSegWords * sizeof(WordT) / (32 * 16));
   static constexpr uint32_t kWordsPerVec = 16 / sizeof(WordT);
+  static constexpr uint32_t kHalfStreams = enc::kWaves * K * S * 2;
 };
 
+// One ANS stream of one block pair.  All but x are wave-uniform.
 struct EStream {
-  uint32_t x;             // state
-  uint32_t nout;          // half-uniform: words emitted so far
-  gp<uint16_t> out;       // slot data of this half's block
+  uint32_t x;              // this lane's state
+  lp<uint16_t> ring;       // output ring of half 0 (half 1 follows)
+  lp<uint16_t> ringLane;   // this lane's half ring
+  int32_t nout[2];         // per half: words emitted so far
+  int32_t flushed[2];      // per half: words already in the slot
+  gp<uint16_t> out[2];     // per half: slot data
 };
+
+// Flush 256 ring words of each half with >= kAt words pending.  Called with
+// kAt = 256 at segment boundaries (before the next segment's loads are
+// issued, so waits for those loads never drain fresh stores) and with
+// kAt = 384 every kUnroll steps (only dense data gets there; it keeps the
+// ring from overflowing: pending <= 383 + 128 < 512).
+template <int kAt>
+__device__ __forceinline__ void ringFlush(EStream& p, uint32_t lane) {
+#pragma unroll
+  for (int hh = 0; hh < 2; ++hh) {
+    if (p.nout[hh] - p.flushed[hh] >= kAt) {
+      const int32_t a = p.flushed[hh] + int32_t(4 * lane);
+      *(gp<u32x2>)(p.out[hh] + a) = *(lp<const u32x2>)(p.ring + hh * enc::kRing + (a & (enc::kRing - 1)));
+      p.flushed[hh] += enc::kFlush;
+    }
+  }
+}
+
+// Flush everything left (whole 4-word groups; the slot has room for them).
+__device__ __forceinline__ void ringFlushAll(EStream& p, uint32_t lane) {
+#pragma unroll
+  for (int hh = 0; hh < 2; ++hh) {
+    for (int32_t a0 = p.flushed[hh]; a0 < p.nout[hh]; a0 += int32_t(enc::kFlush)) {
+      const int32_t a = a0 + int32_t(4 * lane);
+      if (a < p.nout[hh])
+        *(gp<u32x2>)(p.out[hh] + a) = *(lp<const u32x2>)(p.ring + hh * enc::kRing + (a & (enc::kRing - 1)));
+    }
+    p.flushed[hh] = p.nout[hh];
+  }
+}
 
 // One rANS encode step (encodeOneWarp, ans/GpuANSEncode.cuh:49-90) of one
-// stream for both half-waves; writers emit in ascending lane order.
+// stream of a block pair, given the symbol's table entry e; writers emit in
+// ascending lane order.  hv: all-ones on lanes 32-63 (opaque to the
+// compiler).  Masked (!valid) lanes neither write nor change state.
 template <bool kMask>
-__device__ __forceinline__ void encStep(EStream& s, bool valid, uint32_t sym,
-                                        const uint4* __restrict__ tbl, uint32_t h) {
-  const uint4 e = tbl[sym];
-  bool wr = s.x >= e.x;
-  if (kMask) wr = wr && valid;
+__device__ __forceinline__ void encStep(EStream& p, bool valid, const u32x4& e, uint32_t hv,
+                                        uint32_t trashAddr) {
+  const bool wr = kMask ? (valid && p.x >= e.x) : (p.x >= e.x);
   const uint64_t vote = ballot(wr);
-  const uint32_t cLo = uint32_t(__popc(uint32_t(vote)));
-  const uint32_t cHi = uint32_t(__popc(uint32_t(vote >> 32)));
-  uint32_t x = s.x;
-  if (wr) {
-    const uint32_t base = s.nout - (h ? cLo : 0u);
-    s.out[base + mbcnt(vote)] = uint16_t(x);
-    x >>= kEncodedBits;
-  }
-  s.nout += h ? cHi : cLo;
+  const int32_t cLo = __popc(uint32_t(vote));
+  const int32_t cHi = __popc(uint32_t(vote >> 32));
+  // write index = nout + (#writers of my half below me); v_mbcnt over 64
+  // lanes counts every low-half writer for lanes 32-63.
+  const int32_t diff = p.nout[1] - cLo - p.nout[0];
+  const uint32_t vbase = uint32_t(p.nout[0]) + (hv & uint32_t(diff));
+  p.nout[0] += cLo;
+  p.nout[1] += cHi;
+  const uint32_t idx = __builtin_amdgcn_mbcnt_hi(uint32_t(vote >> 32),
+                                                 __builtin_amdgcn_mbcnt_lo(uint32_t(vote), vbase));
+  const uint32_t ringAddr = uint32_t(size_t(p.ringLane + (idx & (enc::kRing - 1))));
+  // non-writers store to their trash dword: one v_cndmask on the ballot mask
+  // and an unconditional ds_write, no exec-mask split of the step
+  uint32_t dst;
+  asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(dst) : "v"(trashAddr), "v"(ringAddr), "s"(vote));
+  *(lp<uint16_t>)size_t(dst) = uint16_t(p.x);
+  const uint32_t x = wr ? (p.x >> kEncodedBits) : p.x;
   uint32_t q = __umulhi(x, e.y);
   q = (q + x) >> (e.w >> 24);
-  const uint32_t xn = __umul24(q, e.w) + x + e.z;
-  s.x = (!kMask || valid) ? xn : x;
+  const uint32_t xn = __umul24(q, e.w) + x + e.z;  // u24 ignores the shift byte
+  p.x = (!kMask || valid) ? xn : x;
 }
 
 // Split 16 B of input words: ANS symbols -> LDS (sym0 / sym1), raw remainder
-// -> the archive raw section at word index i0.
+// -> the archive raw section at word index i0 (splitFloat's per-word split,
+// float/GpuFloatCompress.cuh:423-551; FloatTypeInfo::split,
+// float/GpuFloatUtils.cuh:190-370).
 template <int FT>
 __device__ __forceinline__ void splitVec(const uint4& v, uint32_t i0, uint32_t n,
-                                         gp<uint8_t> raw, uint8_t* sym0, uint8_t* sym1) {
+                                         gp<uint8_t> raw, lp<uint8_t> sym0, lp<uint8_t> sym1) {
   using WordT = typename FloatTraits<FT>::WordT;
   const WordT* ws = reinterpret_cast<const WordT*>(&v);
   if constexpr (FT == 0) {
-    *reinterpret_cast<uint4*>(sym0) = v;
+    *(lp<u32x4>)sym0 = u32x4{v.x, v.y, v.z, v.w};
   } else if constexpr (FT == 1 || FT == 2) {
-    uint32_t e0 = 0, e1 = 0, r0 = 0, r1 = 0;
+    // words (lo, hi) of each dword; exponent / raw bytes gathered with v_perm
+    const uint32_t dw[4] = {v.x, v.y, v.z, v.w};
+    uint32_t t[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      const uint32_t a = ws[k], c = ws[k + 4];
-      if constexpr (FT == 1) {
-        e0 |= (a >> 8) << (8 * k);
-        e1 |= (c >> 8) << (8 * k);
-        r0 |= (a & 0xffu) << (8 * k);
-        r1 |= (c & 0xffu) << (8 * k);
-      } else {
-        e0 |= ((a >> 7) & 0xffu) << (8 * k);
-        e1 |= ((c >> 7) & 0xffu) << (8 * k);
-        r0 |= (((a << 1) | (a >> 15)) & 0xffu) << (8 * k);
-        r1 |= (((c << 1) | (c >> 15)) & 0xffu) << (8 * k);
-      }
+      // bf16: rotate each half left by one so that [exp | raw] are the bytes
+      t[k] = FT == 1 ? dw[k] : (((dw[k] << 1) & 0xfffefffeu) | ((dw[k] >> 15) & 0x00010001u));
     }
-    *reinterpret_cast<uint2*>(sym0) = make_uint2(e0, e1);
+    const uint32_t e0 = __builtin_amdgcn_perm(t[1], t[0], 0x07050301u);
+    const uint32_t e1 = __builtin_amdgcn_perm(t[3], t[2], 0x07050301u);
+    const uint32_t r0 = __builtin_amdgcn_perm(t[1], t[0], 0x06040200u);
+    const uint32_t r1 = __builtin_amdgcn_perm(t[3], t[2], 0x06040200u);
+    *(lp<u32x2>)sym0 = u32x2{e0, e1};
     st8(raw + i0, make_uint2(r0, r1));
   } else if constexpr (FT == 3) {
-    uint32_t e = 0, hb = 0, lo[4];
+    uint32_t r[4];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const uint32_t r = rotl32(ws[k], 1);
-      e |= (r >> 24) << (8 * k);
-      hb |= ((r >> 16) & 0xffu) << (8 * k);
-      lo[k] = r & 0xffffu;
-    }
-    *reinterpret_cast<uint32_t*>(sym0) = e;
-    st8(raw + 2 * i0, make_uint2(lo[0] | (lo[1] << 16), lo[2] | (lo[3] << 16)));
-    *(gp<uint32_t>)(raw + 2 * roundUp(n, 8) + i0) = hb;
+    for (int k = 0; k < 4; ++k) r[k] = rotl32(ws[k], 1);
+    *(lp<uint32_t>)sym0 = __builtin_amdgcn_perm(r[1], r[0], 0x07030703u) & 0xffffu |
+                          (__builtin_amdgcn_perm(r[3], r[2], 0x07030703u) << 16);
+    st8(raw + 2 * i0, make_uint2(__builtin_amdgcn_perm(r[1], r[0], 0x05040100u),
+                                 __builtin_amdgcn_perm(r[3], r[2], 0x05040100u)));
+    *(gp<uint32_t>)(raw + 2 * roundUp(n, 8) + i0) =
+        __builtin_amdgcn_perm(r[1], r[0], 0x06020602u) & 0xffffu |
+        (__builtin_amdgcn_perm(r[3], r[2], 0x06020602u) << 16);
   } else {
     const uint64_t r0 = rotl64(ws[0], 1), r1 = rotl64(ws[1], 1);
-    *reinterpret_cast<uint16_t*>(sym0) = uint16_t((r0 >> 56) | ((r1 >> 56) << 8));
-    *reinterpret_cast<uint16_t*>(sym1) = uint16_t(((r0 >> 48) & 0xffu) | (((r1 >> 48) & 0xffu) << 8));
+    *(lp<uint16_t>)sym0 = uint16_t((r0 >> 56) | ((r1 >> 56) << 8));
+    *(lp<uint16_t>)sym1 = uint16_t(((r0 >> 48) & 0xffu) | (((r1 >> 48) & 0xffu) << 8));
     st8(raw + 4 * i0, make_uint2(uint32_t(r0), uint32_t(r1)));
     *(gp<uint32_t>)(raw + 4 * roundUp(n, 4) + 2 * i0) =
         uint32_t((r0 >> 32) & 0xffffu) | (uint32_t((r1 >> 32) & 0xffffu) << 16);
@@ -305,7 +355,7 @@ __device__ __forceinline__ void splitVec(const uint4& v, uint32_t i0, uint32_t n
 // scalar split of one word (unaligned input or element tail)
 template <int FT>
 __device__ __forceinline__ void splitOne(typename FloatTraits<FT>::WordT w, uint32_t i, uint32_t n,
-                                         gp<uint8_t> raw, uint8_t* sym0, uint8_t* sym1) {
+                                         gp<uint8_t> raw, lp<uint8_t> sym0, lp<uint8_t> sym1) {
   if constexpr (FT == 0) {
     *sym0 = w;
   } else if constexpr (FT == 1) {
@@ -328,6 +378,8 @@ __device__ __forceinline__ void splitOne(typename FloatTraits<FT>::WordT w, uint
   }
 }
 
+// grid (ceil(MB / kBlocksPerWG), batch).  Writes per block: slot states,
+// slot words and cw[] (word count).
 template <int FT>
 __global__ __launch_bounds__(enc::kThreads) void k_encode(BatchDesc in, BatchDesc out,
                                                           uint32_t batchOffset,
@@ -338,126 +390,200 @@ __global__ __launch_bounds__(enc::kThreads) void k_encode(BatchDesc in, BatchDes
   using Cfg = EncCfg<FT>;
   using WordT = typename Cfg::WordT;
   constexpr int S = Cfg::S, K = Cfg::K, V = Cfg::V;
-  __shared__ uint4 tbl[S][kNumSymbols];
-  __shared__ __attribute__((aligned(16))) uint8_t symBuf[enc::kWaves][K][S][2][enc::kSegWords];
+  __shared__ __attribute__((aligned(16))) uint32_t tblS[S][kNumSymbols * 4];
+  __shared__ __attribute__((aligned(16))) uint8_t symS[Cfg::kHalfStreams][enc::kSegWords];
+  __shared__ __attribute__((aligned(16))) uint16_t ringS[Cfg::kHalfStreams / 2][2 * enc::kRing];
+  __shared__ uint32_t trashS[enc::kWaves][64];
 
   const uint32_t b = batchOffset + blockIdx.y;
   const uint32_t tid = threadIdx.x;
+#pragma unroll
   for (int s = 0; s < S; ++s) {
-    for (uint32_t i = tid; i < kNumSymbols; i += enc::kThreads)
-      tbl[s][i] = ld16(G(table) + (uint64_t(s) * numInBatch + b) * kNumSymbols + i);
+    const uint4 t = ld16(G(table) + (uint64_t(s) * numInBatch + b) * kNumSymbols + tid);
+    *(lp<u32x4>)&tblS[s][4 * tid] = u32x4{t.x, t.y, t.z, t.w};
   }
   __syncthreads();
 
   const uint32_t n = in.size(b);
   const uint32_t nBlocks = divUp(n, kBlockSize);
-  const uint32_t w = tid >> 6, lane = tid & 63, h = lane >> 5, l = lane & 31;
+  const uint32_t w = readfirst(tid >> 6), lane = tid & 63, h = lane >> 5, l = lane & 31;
   const uint32_t blk0 = blockIdx.x * Cfg::kBlocksPerWG + w * Cfg::kBlocksPerWave;
   if (blk0 >= nBlocks) return;
+  uint32_t hv = h ? ~0u : 0u;
+  asm volatile("" : "+v"(hv));  // keep `hv & x` a v_and
 
   gp<const WordT> src = (gp<const WordT>)startOf(in, b);
   gp<uint8_t> raw = FT == 0 ? gp<uint8_t>(nullptr) : startOf(out, b) + 32;
   const bool vecIn = (reinterpret_cast<uintptr_t>(src) & 15) == 0;
+  const uint32_t trashAddr = uint32_t(size_t((lp<uint32_t>)&trashS[w][lane]));
 
+  uint32_t uwH[K][2];  // wave-uniform
   uint32_t blk[K], uw[K];
   EStream st[K][S];
+  lp<uint8_t> symLane[K][S];
 #pragma unroll
   for (int c = 0; c < K; ++c) {
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      const uint32_t bk = blk0 + 2 * c + hh;
+      uwH[c][hh] = bk < nBlocks ? min(kBlockSize, n - bk * kBlockSize) : 0u;
+    }
     blk[c] = blk0 + 2 * c + h;
-    uw[c] = blk[c] < nBlocks ? min(kBlockSize, n - blk[c] * kBlockSize) : 0u;
-    const uint32_t sb = blk[c] < nBlocks ? blk[c] : blk0;
+    uw[c] = h ? uwH[c][1] : uwH[c][0];
 #pragma unroll
     for (int s = 0; s < S; ++s) {
-      st[c][s].x = kStartState;
-      st[c][s].nout = 0;
-      st[c][s].out = (gp<uint16_t>)(G(slots) + ((uint64_t(s) * numInBatch + b) * MB + sb) * kSlotBytes +
-                                    kStateBytesPerBlock);
+      EStream& p = st[c][s];
+      const uint32_t hs = (w * K + c) * S + s;
+      p.x = kStartState;
+      p.ring = (lp<uint16_t>)&ringS[hs][0];
+      p.ringLane = p.ring + (hv & enc::kRing);
+      symLane[c][s] = (lp<uint8_t>)&symS[2 * hs][0] + (hv & enc::kSegWords) + l;
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        const uint32_t bk = blk0 + 2 * c + hh;
+        const uint32_t sb = bk < nBlocks ? bk : blk0;
+        p.nout[hh] = 0;
+        p.flushed[hh] = 0;
+        p.out[hh] = (gp<uint16_t>)(G(slots) + ((uint64_t(s) * numInBatch + b) * MB + sb) * kSlotBytes +
+                                   kStateBytesPerBlock);
+      }
     }
   }
   uint32_t T = 0;
 #pragma unroll
-  for (int c = 0; c < K; ++c) {
-    const uint32_t tc = divUp(uw[c], 32);
-    T = max(T, max(__builtin_amdgcn_readlane(tc, 0), __builtin_amdgcn_readlane(tc, 32)));
-  }
-  const uint32_t nSeg = divUp(T, 32);
+  for (int c = 0; c < K; ++c) T = max(T, max(divUp(uwH[c][0], 32), divUp(uwH[c][1], 32)));
+  const uint32_t nSeg = divUp(T, enc::kSegSteps);
 
-  // prefetch segment 0
-  uint4 pv[K][V];
-  auto loadSeg = [&](uint32_t g) {
+  lp<const u32x4> tbl[S];
 #pragma unroll
-    for (int c = 0; c < K; ++c) {
-#pragma unroll
-      for (int k = 0; k < V; ++k) {
-        const uint32_t j0 = g * enc::kSegWords + (k * 32 + l) * Cfg::kWordsPerVec;
-        if (vecIn && j0 + Cfg::kWordsPerVec <= uw[c])
-          pv[c][k] = ld16(src + blk[c] * kBlockSize + j0);
-      }
-    }
-  };
-  loadSeg(0);
+  for (int s = 0; s < S; ++s) tbl[s] = (lp<const u32x4>)&tblS[s][0];
 
-  for (uint32_t g = 0; g < nSeg; ++g) {
-    const uint32_t segW0 = g * enc::kSegWords;
-    // split this segment: symbols -> LDS, raw -> archive
+  // segments [0, nFull) are full for every block of the wave
+  uint32_t nFull = ~0u;
 #pragma unroll
-    for (int c = 0; c < K; ++c) {
-      if (uw[c] <= segW0) continue;
-      const uint32_t segCnt = min(enc::kSegWords, uw[c] - segW0);
+  for (int c = 0; c < K; ++c)
+    nFull = min(nFull, min(uwH[c][0], uwH[c][1]) / enc::kSegWords);
+
+  // kVec: 16 B aligned input (chosen once per wave).  With it, full
+  // segments split unconditionally, so the prefetch registers are always
+  // consumed before they are reloaded (no vmcnt(0) drain of the stores).
+  auto run = [&](auto vecTag) {
+    constexpr bool kVec = decltype(vecTag)::value;
+    uint4 pv[K][V];  // input vectors, one segment ahead
+    auto loadSeg = [&](uint32_t g) {
 #pragma unroll
-      for (int k = 0; k < V; ++k) {
-        const uint32_t off = (k * 32 + l) * Cfg::kWordsPerVec;  // word offset in segment
-        uint8_t* s0 = &symBuf[w][c][0][h][off];
-        uint8_t* s1 = &symBuf[w][c][S - 1][h][off];
-        const uint32_t i0 = blk[c] * kBlockSize + segW0 + off;
-        if (vecIn && off + Cfg::kWordsPerVec <= segCnt) {
-          splitVec<FT>(pv[c][k], i0, n, raw, s0, s1);
-        } else {
-          for (uint32_t q = 0; q < Cfg::kWordsPerVec && off + q < segCnt; ++q)
-            splitOne<FT>(src[i0 + q], i0 + q, n, raw, s0 + q, s1 + q);
+      for (int c = 0; c < K; ++c) {
+#pragma unroll
+        for (int k = 0; k < V; ++k) {
+          const uint32_t j0 = g * enc::kSegWords + (k * 32 + l) * Cfg::kWordsPerVec;
+          if (kVec && (g < nFull || j0 + Cfg::kWordsPerVec <= uw[c]))
+            pv[c][k] = ld16(src + blk[c] * kBlockSize + j0);
         }
       }
-    }
-    if (g + 1 < nSeg) loadSeg(g + 1);
-
-    bool full = true;
+    };
+    // split segment g: symbols -> LDS, raw -> archive
+    auto split = [&](uint32_t g, bool fullSeg) {
+      const uint32_t segW0 = g * enc::kSegWords;
 #pragma unroll
-    for (int c = 0; c < K; ++c) full = full && uw[c] >= segW0 + enc::kSegWords;
-    full = ballot(full) == ~0ull;
-    const uint32_t tEnd = min(T, (g + 1) * 32);
-    if (full) {
-#pragma unroll 4
-      for (uint32_t t = g * 32; t < tEnd; ++t) {
-        const uint32_t si = (t - g * 32) * 32 + l;
+      for (int c = 0; c < K; ++c) {
+        if (!fullSeg && uw[c] <= segW0) continue;
+        const uint32_t segCnt = fullSeg ? enc::kSegWords : min(enc::kSegWords, uw[c] - segW0);
+#pragma unroll
+        for (int k = 0; k < V; ++k) {
+          const uint32_t off = (k * 32 + l) * Cfg::kWordsPerVec;  // word offset in segment
+          lp<uint8_t> s0 = symLane[c][0] - l + off;
+          lp<uint8_t> s1 = symLane[c][S - 1] - l + off;
+          const uint32_t i0 = blk[c] * kBlockSize + segW0 + off;
+          if (kVec && (fullSeg || off + Cfg::kWordsPerVec <= segCnt)) {
+            splitVec<FT>(pv[c][k], i0, n, raw, s0, s1);
+          } else {
+            for (uint32_t q = 0; q < Cfg::kWordsPerVec && off + q < segCnt; ++q)
+              splitOne<FT>(src[i0 + q], i0 + q, n, raw, s0 + q, s1 + q);
+          }
+        }
+      }
+    };
+
+    if (nSeg > 0) loadSeg(0);
+    for (uint32_t g = 0; g < nFull; ++g) {
+      split(g, true);
+#pragma unroll
+      for (int c = 0; c < K; ++c)
+#pragma unroll
+        for (int s = 0; s < S; ++s) ringFlush<256>(st[c][s], lane);
+      if (g + 1 < nSeg) loadSeg(g + 1);
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int grp = 0; grp < int(enc::kSegSteps / enc::kUnroll); ++grp) {
 #pragma unroll
         for (int c = 0; c < K; ++c)
 #pragma unroll
-          for (int s = 0; s < S; ++s) encStep<false>(st[c][s], true, symBuf[w][c][s][h][si], tbl[s], h);
+          for (int s = 0; s < S; ++s) ringFlush<384>(st[c][s], lane);
+        // the group's symbols and table entries first: their LDS reads
+        // cannot be hoisted over the ring stores of earlier steps
+        u32x4 E[enc::kUnroll][K][S];
+#pragma unroll
+        for (int u = 0; u < int(enc::kUnroll); ++u)
+#pragma unroll
+          for (int c = 0; c < K; ++c)
+#pragma unroll
+            for (int s = 0; s < S; ++s)
+              E[u][c][s] = tbl[s][symLane[c][s][(grp * int(enc::kUnroll) + u) * 32]];
+#pragma unroll
+        for (int u = 0; u < int(enc::kUnroll); ++u)
+#pragma unroll
+          for (int c = 0; c < K; ++c)
+#pragma unroll
+            for (int s = 0; s < S; ++s) encStep<false>(st[c][s], true, E[u][c][s], hv, trashAddr);
       }
-    } else {
-      for (uint32_t t = g * 32; t < tEnd; ++t) {
-        const uint32_t si = (t - g * 32) * 32 + l;
+      __builtin_amdgcn_wave_barrier();
+    }
+    // partial segments (element tail / odd block counts): masked steps
+    for (uint32_t g = nFull; g < nSeg; ++g) {
+      split(g, false);
+#pragma unroll
+      for (int c = 0; c < K; ++c)
+#pragma unroll
+        for (int s = 0; s < S; ++s) ringFlush<256>(st[c][s], lane);
+      if (g + 1 < nSeg) loadSeg(g + 1);
+      __builtin_amdgcn_wave_barrier();
+      const uint32_t tEnd = min(T, (g + 1) * enc::kSegSteps);
+      for (uint32_t t = g * enc::kSegSteps; t < tEnd; ++t) {
+#pragma unroll
+        for (int c = 0; c < K; ++c)
+#pragma unroll
+          for (int s = 0; s < S; ++s) ringFlush<int(512 - 32)>(st[c][s], lane);
+        const uint32_t tr = t - g * enc::kSegSteps;
 #pragma unroll
         for (int c = 0; c < K; ++c) {
           const bool valid = t * 32 + l < uw[c];
 #pragma unroll
           for (int s = 0; s < S; ++s) {
-            const uint32_t sym = valid ? uint32_t(symBuf[w][c][s][h][si]) : 0u;
-            encStep<true>(st[c][s], valid, sym, tbl[s], h);
+            const uint32_t sym = valid ? uint32_t(symLane[c][s][tr * 32]) : 0u;
+            const u32x4 e = tbl[s][sym];
+            encStep<true>(st[c][s], valid, e, hv, trashAddr);
           }
         }
       }
+      __builtin_amdgcn_wave_barrier();
     }
-  }
+  };
+  if (vecIn)
+    run(std::true_type{});
+  else
+    run(std::false_type{});
 
 #pragma unroll
   for (int c = 0; c < K; ++c) {
-    if (!uw[c]) continue;
 #pragma unroll
     for (int s = 0; s < S; ++s) {
-      gp<uint8_t> slot = G(slots) + ((uint64_t(s) * numInBatch + b) * MB + blk[c]) * kSlotBytes;
-      ((gp<uint32_t>)slot)[l] = st[c][s].x;
-      if (l == 0) G(cw)[(uint64_t(s) * numInBatch + b) * MB + blk[c]] = st[c][s].nout;
+      EStream& p = st[c][s];
+      ringFlushAll(p, lane);
+      if (uw[c]) {
+        gp<uint8_t> slot = G(slots) + ((uint64_t(s) * numInBatch + b) * MB + blk[c]) * kSlotBytes;
+        ((gp<uint32_t>)slot)[l] = p.x;
+        if (l == 0) G(cw)[(uint64_t(s) * numInBatch + b) * MB + blk[c]] = uint32_t(h ? p.nout[1] : p.nout[0]);
+      }
     }
   }
 }
