@@ -38,7 +38,8 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-sample", type=int, default=256,
                    help="tensors of the batch timed on the CPU oracle (rank 0, N=1)")
-    p.add_argument("--verify", action="store_true", default=True)
+    p.add_argument("--no-verify", dest="verify", action="store_false",
+                   help="skip the round-trip check (kernel-variant timing experiments only)")
     return p.parse_args()
 
 

@@ -32,6 +32,15 @@ uint32_t histChunkWords(uint32_t nb, uint32_t maxSize) {
   return chunk;
 }
 
+// workgroups of `kernel` resident on the whole device at once
+uint32_t residentSlots(const void* kernel, int threads, uint32_t dynLds) {
+  int dev = 0, cus = 0, perCU = 0;
+  HIP_CHECK(hipGetDevice(&dev));
+  HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, kernel, threads, dynLds));
+  return uint32_t(std::max(1, cus) * std::max(1, perCU));
+}
+
 void checkProbBits(int pb) {
   DG_CHECK(pb >= 9 && pb <= 11, "unhandled pdf precision " << pb << " (must be 9, 10 or 11)");
 }
@@ -125,9 +134,13 @@ void decodeBatchDevice(StackDeviceMemory& res, int pb, uint32_t nb, const BatchD
   for (uint32_t y0 = 0; y0 < nb; y0 += kMaxGridY) {
     const uint32_t ny = std::min(kMaxGridY, nb - y0);
     prof::Scope p("decode", s);
-    dim3 g(std::max(1u, divUp(maxBlocks, DecCfg<FT>::kBlocksPerWG)), ny);
-    k_decode<FT><<<g, dec::kThreads, DecCfg<FT>::ldsBytes(pb), s>>>(in, out, y0, pb,
-                                                                    outSuccess_dev, outSize_dev);
+    // one generation of resident workgroups; each decodes P chunks
+    const uint32_t lds = DecCfg<FT>::ldsBytes(pb);
+    const uint32_t chunks = std::max(1u, divUp(maxBlocks, DecCfg<FT>::kBlocksPerWG));
+    const uint32_t slots = residentSlots(reinterpret_cast<const void*>(&k_decode<FT>), dec::kThreads, lds);
+    const uint32_t P = std::max(1u, uint32_t((uint64_t(chunks) * ny + slots / 2) / slots));
+    dim3 g(divUp(chunks, P), ny);
+    k_decode<FT><<<g, dec::kThreads, lds, s>>>(in, out, y0, pb, P, outSuccess_dev, outSize_dev);
     HIP_LAUNCH_CHECK();
   }
 }
@@ -589,3 +602,11 @@ void floatGetCompressedInfo(StackDeviceMemory& res, const void** in, uint32_t nu
 }
 
 }  // namespace dietgpu
+
+#if DG_EXP == 7
+extern "C" int dietgpu_debug_read(void* dst, size_t bytes) {
+  return hipMemcpyFromSymbol(dst, HIP_SYMBOL(dietgpu::g_dbgT), bytes, 0, hipMemcpyDeviceToHost) == hipSuccess
+             ? 0
+             : 2;
+}
+#endif

@@ -24,9 +24,29 @@
 //    issued before the segment) and written with 16 B stores.
 #pragma once
 
+#include <type_traits>
+
 #include "device.h"
 
+#ifndef DG_EXP
+#define DG_EXP 0  // timing experiments only (make exp): 0 = the real decoder
+#endif
+
 namespace dietgpu {
+#if DG_EXP == 7
+// experiment 7: per-wave s_memtime stamps (lane 0), 24 slots per wave
+__device__ uint64_t g_dbgT[16384 * 24];
+#define DG_STAMP(slot)                                                                \
+  do {                                                                                \
+    if (lane == 0 && blockIdx.y * gridDim.x * 4 < 16384)                              \
+      g_dbgT[((blockIdx.y * gridDim.x + blockIdx.x) * 4 + w) * 24 + (slot)] =         \
+          __builtin_amdgcn_s_memtime();                                               \
+  } while (0)
+#else
+#define DG_STAMP(slot) \
+  do {                 \
+  } while (0)
+#endif
 namespace dec {
 constexpr int kThreads = 256;
 constexpr int kWaves = kThreads / 64;
@@ -78,17 +98,21 @@ __device__ __forceinline__ void ringPrefetch(DStream& p, int hh, uint32_t lane, 
     p.pf[hh] = ld4w(p.data[hh] + nlo + 4 * lane, vec);
 }
 
-// Keep the next kUnroll steps' words of both halves in the ring.
-__device__ __forceinline__ void ringEnsure(DStream& p, uint32_t lane, bool vec) {
+// Refill [lo - 256, lo) of each half from its prefetch registers when fewer
+// than kAt words are buffered below ptr (the refill overwrites words
+// >= lo + 256, all consumed since ptr < lo + kAt <= lo + 256).  kAt = 256 at
+// segment boundaries; kAt = 32 * kUnroll every kUnroll steps as the
+// emergency path for dense data (then the next prefetch is issued at once).
+template <int kAt, bool kPrefetchNow>
+__device__ __forceinline__ void ringRefill(DStream& p, uint32_t lane, bool vec) {
 #pragma unroll
   for (int hh = 0; hh < 2; ++hh) {
-    if (p.lo[hh] > 0 && p.ptr[hh] - int32_t(32 * dec::kUnroll) < p.lo[hh]) {
-      // the refill overwrites words >= lo + 256, all consumed (ptr < lo + 128)
+    if (DG_EXP != 3 && p.lo[hh] > 0 && p.ptr[hh] - kAt < p.lo[hh]) {
       const int32_t nlo = max(0, p.lo[hh] - int32_t(dec::kRefill));
       if (int32_t(4 * lane) < p.lo[hh] - nlo)
         *(lp<u32x2>)(p.ring + hh * dec::kRing + ((nlo + 4 * lane) & (dec::kRing - 1))) = p.pf[hh];
       p.lo[hh] = nlo;
-      ringPrefetch(p, hh, lane, vec);
+      if (kPrefetchNow) ringPrefetch(p, hh, lane, vec);
     }
   }
 }
@@ -116,7 +140,11 @@ __device__ __forceinline__ uint32_t decStep(DStream& p, bool valid, lp<const u32
   const uint32_t vbase = uint32_t(baseLo) + (hv & uint32_t(diff));
   const uint32_t idx = __builtin_amdgcn_mbcnt_hi(uint32_t(vote >> 32),
                                                  __builtin_amdgcn_mbcnt_lo(uint32_t(vote), vbase));
+#if DG_EXP == 2
+  const uint32_t v = idx;  // experiment: no ring read
+#else
   const uint32_t v = p.ringLane[idx & (dec::kRing - 1)];  // harmless for non-readers
+#endif
   // x = rd ? (xn << 16 | v) : xn as one v_perm.  Feeding the word through an
   // intrinsic (not a select) keeps the LDS read unconditional: a branch
   // around it would split the step and serialise the independent chains.
@@ -253,12 +281,13 @@ __device__ __forceinline__ void buildLut64(gp<const uint16_t> pdfIn, lp<u32x2> l
   }
 }
 
-// grid (ceil(maxBlocks / kBlocksPerWG), batch), dynamic LDS
+// grid (ceil(maxBlocks / (kBlocksPerWG * chunksPerWG)), batch), dynamic LDS
 // DecCfg<FT>::ldsBytes(pb).  out.size(b) = capacity (bytes for raw ANS,
 // words for floats).
 template <int FT>
 __global__ __launch_bounds__(dec::kThreads) void k_decode(BatchDesc in, BatchDesc out,
                                                           uint32_t batchOffset, int pb,
+                                                          uint32_t chunksPerWG,
                                                           uint8_t* __restrict__ outSuccess,
                                                           uint32_t* __restrict__ outSize) {
   using Cfg = DecCfg<FT>;
@@ -299,7 +328,7 @@ __global__ __launch_bounds__(dec::kThreads) void k_decode(BatchDesc in, BatchDes
     if (outSize) outSize[b] = ok ? n : 0u;
   }
   const uint32_t nBlocks = divUp(n, kBlockSize);
-  if (!success || blockIdx.x * Cfg::kBlocksPerWG >= nBlocks) return;
+  if (!success || blockIdx.x * chunksPerWG * Cfg::kBlocksPerWG >= nBlocks) return;
 
 #pragma unroll
   for (int s = 0; s < S; ++s) {
@@ -311,8 +340,15 @@ __global__ __launch_bounds__(dec::kThreads) void k_decode(BatchDesc in, BatchDes
   const uint32_t w = readfirst(tid >> 6), lane = tid & 63, l = lane & 31;
   uint32_t hv = lane >= 32 ? ~0u : 0u;
   asm volatile("" : "+v"(hv));  // keep `hv & x` a v_and (not a v_cndmask pair)
-  const uint32_t blk0 = blockIdx.x * Cfg::kBlocksPerWG + w * Cfg::kBlocksPerWave;
-  if (blk0 >= nBlocks) return;
+  DG_STAMP(0);
+#if DG_EXP == 7
+  if (lane == 0 && blockIdx.y * gridDim.x * 4 < 16384)
+    g_dbgT[((blockIdx.y * gridDim.x + blockIdx.x) * 4 + w) * 24 + 23] =
+        __builtin_amdgcn_s_getreg((4) | (0 << 6) | (31 << 11)) |
+        (uint64_t(__builtin_amdgcn_s_getreg((20) | (0 << 6) | (31 << 11))) << 32);
+  if (lane == 0 && blockIdx.y * gridDim.x * 4 < 16384)
+    g_dbgT[((blockIdx.y * gridDim.x + blockIdx.x) * 4 + w) * 24 + 22] = __builtin_amdgcn_s_memrealtime();
+#endif
 
   const bool vecIn = (reinterpret_cast<uintptr_t>(base) & 15) == 0;
   gp<uint8_t> outB = startOf(out, b);
@@ -320,152 +356,218 @@ __global__ __launch_bounds__(dec::kThreads) void k_decode(BatchDesc in, BatchDes
   gp<const uint8_t> raw = base + 32;
   const uint32_t mask = (1u << pb) - 1;
 
-  // per pair c: blocks blk0 + 2c (lanes 0-31) and blk0 + 2c + 1 (lanes 32-63)
-  uint32_t uwH[K][2];  // wave-uniform
-  DStream st[K][S];
-  lp<uint16_t> segLane[K][S];
-#pragma unroll
-  for (int c = 0; c < K; ++c) {
-#pragma unroll
-    for (int s = 0; s < S; ++s) {
-      gp<const uint8_t> states = arch[s] + kANSHeaderBytes + kPdfBytes;
-      gp<const uint2> bw = (gp<const uint2>)(states + uint64_t(kStateBytesPerBlock) * nBlocks);
-      gp<const uint16_t> data = (gp<const uint16_t>)(bw + roundUp(nBlocks, 2));
-      DStream& d = st[c][s];
-      const uint32_t hs = (w * K + c) * S + s;  // half-stream pair index
-      d.ring = ringAll + hs * 2 * dec::kRing;
-      d.ringLane = d.ring + (hv & dec::kRing);
-      segLane[c][s] = segAll + hs * 2 * dec::kSegWords + (hv & dec::kSegWords) + l;
-#pragma unroll
-      for (int hh = 0; hh < 2; ++hh) {
-        const uint32_t bk = blk0 + 2 * c + hh;
-        uwH[c][hh] = 0;
-        d.ptr[hh] = 0;
-        d.lo[hh] = 0;
-        d.data[hh] = data;
-        d.pf[hh] = u32x2{0, 0};
-        if (bk < nBlocks) {
-          const uint2 e = ld8(bw + bk);
-          uwH[c][hh] = e.x >> 16;
-          const int32_t cw = int32_t(e.x & 0xffffu);
-          d.ptr[hh] = cw;
-          d.data[hh] = data + e.y;
-          const int32_t lo = cw > int32_t(dec::kRing) ? int32_t(roundUp(uint32_t(cw) - dec::kRing, 4)) : 0;
-          d.lo[hh] = lo;
-          // initial fill of [lo, cw) (<= 512 words: two wave-wide passes)
-#pragma unroll
-          for (int q = 0; q < 2; ++q) {
-            const int32_t a = lo + q * int32_t(dec::kRefill) + int32_t(4 * lane);
-            if (a < cw)
-              *(lp<u32x2>)(d.ring + hh * dec::kRing + (a & (dec::kRing - 1))) = ld4w(d.data[hh] + a, vecIn);
-          }
-          ringPrefetch(d, hh, lane, vecIn);
-        }
-      }
-      const uint32_t bkMine = blk0 + 2 * c + (lane >> 5);
-      d.x = bkMine < nBlocks
-                ? ((gp<const uint32_t>)(states + uint64_t(kStateBytesPerBlock) * bkMine))[l]
-                : kMinState;
-    }
-  }
-
-  uint32_t T = 0;
-#pragma unroll
-  for (int c = 0; c < K; ++c) T = max(T, max(divUp(uwH[c][0], 32), divUp(uwH[c][1], 32)));
-
-  lp<const u32x2> lut[S];
-#pragma unroll
-  for (int s = 0; s < S; ++s) lut[s] = (lp<const u32x2>)(L + s * (lutBytes / S));
-
-  for (int32_t g = int32_t(T - 1) / int32_t(dec::kSegSteps); g >= 0; --g) {
-    const uint32_t segW0 = uint32_t(g) * dec::kSegWords;  // first word of segment in block
-    const uint32_t off = 16 * l;                           // this lane's chunk in the segment
-    // prefetch the raw bytes of this segment's chunks
-    uint4 rv[K][R];
-#pragma unroll
+  // Persistent over chunksPerWG consecutive 16-block chunks of this element
+  // (the grid is sized to one generation of resident workgroups, so no
+  // second-generation dip and one table build per workgroup).
+  for (uint32_t pass = 0; pass < chunksPerWG; ++pass) {
+    const uint32_t blk0 = (blockIdx.x * chunksPerWG + pass) * Cfg::kBlocksPerWG + w * Cfg::kBlocksPerWave;
+    if (blk0 >= nBlocks) break;
+    // per pair c: blocks blk0 + 2c (lanes 0-31) and blk0 + 2c + 1 (lanes 32-63)
+    uint32_t uwH[K][2];  // wave-uniform
+    DStream st[K][S];
+    lp<uint16_t> segLane[K][S];
+  #pragma unroll
     for (int c = 0; c < K; ++c) {
-      const uint32_t uw = lane >= 32 ? uwH[c][1] : uwH[c][0];
-      const uint32_t bk = blk0 + 2 * c + (lane >> 5);
-      if (FT != 0 && vecIn && segW0 + off + 16 <= uw)
-        Join<FT>::load(rv[c], raw, n, bk * kBlockSize + segW0 + off);
+  #pragma unroll
+      for (int s = 0; s < S; ++s) {
+        gp<const uint8_t> states = arch[s] + kANSHeaderBytes + kPdfBytes;
+        gp<const uint2> bw = (gp<const uint2>)(states + uint64_t(kStateBytesPerBlock) * nBlocks);
+        gp<const uint16_t> data = (gp<const uint16_t>)(bw + roundUp(nBlocks, 2));
+        DStream& d = st[c][s];
+        const uint32_t hs = (w * K + c) * S + s;  // half-stream pair index
+        d.ring = ringAll + hs * 2 * dec::kRing;
+        d.ringLane = d.ring + (hv & dec::kRing);
+        segLane[c][s] = segAll + hs * 2 * dec::kSegWords + (hv & dec::kSegWords) + l;
+  #pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+          const uint32_t bk = blk0 + 2 * c + hh;
+          uwH[c][hh] = 0;
+          d.ptr[hh] = 0;
+          d.lo[hh] = 0;
+          d.data[hh] = data;
+          d.pf[hh] = u32x2{0, 0};
+          if (bk < nBlocks) {
+            const uint2 e = ld8(bw + bk);
+            const uint32_t ex = readfirst(e.x), ey = readfirst(e.y);  // wave-uniform: SGPRs
+            uwH[c][hh] = ex >> 16;
+            const int32_t cw = int32_t(ex & 0xffffu);
+            d.ptr[hh] = cw;
+            d.data[hh] = data + ey;
+            const int32_t lo = cw > int32_t(dec::kRing) ? int32_t(roundUp(uint32_t(cw) - dec::kRing, 4)) : 0;
+            d.lo[hh] = lo;
+            // initial fill of [lo, cw) (<= 512 words: two wave-wide passes)
+  #pragma unroll
+            for (int q = 0; q < 2; ++q) {
+              const int32_t a = lo + q * int32_t(dec::kRefill) + int32_t(4 * lane);
+              if (a < cw)
+                *(lp<u32x2>)(d.ring + hh * dec::kRing + (a & (dec::kRing - 1))) = ld4w(d.data[hh] + a, vecIn);
+            }
+            ringPrefetch(d, hh, lane, vecIn);
+          }
+        }
+        const uint32_t bkMine = blk0 + 2 * c + (lane >> 5);
+        d.x = bkMine < nBlocks
+                  ? ((gp<const uint32_t>)(states + uint64_t(kStateBytesPerBlock) * bkMine))[l]
+                  : kMinState;
+      }
     }
 
-    bool full = true;
-#pragma unroll
-    for (int c = 0; c < K; ++c)
-      full = full && uwH[c][0] >= segW0 + dec::kSegWords && uwH[c][1] >= segW0 + dec::kSegWords;
+    uint32_t T = 0;
+  #pragma unroll
+    for (int c = 0; c < K; ++c) T = max(T, max(divUp(uwH[c][0], 32), divUp(uwH[c][1], 32)));
 
-    if (full) {
-#pragma unroll
-      for (int grp = int(dec::kSegSteps / dec::kUnroll) - 1; grp >= 0; --grp) {
-#pragma unroll
-        for (int c = 0; c < K; ++c)
-#pragma unroll
-          for (int s = 0; s < S; ++s) ringEnsure(st[c][s], lane, vecIn);
-#pragma unroll
-        for (int u = int(dec::kUnroll) - 1; u >= 0; --u) {
-          const int tr = grp * int(dec::kUnroll) + u;  // step within segment
-#pragma unroll
-          for (int c = 0; c < K; ++c)
-#pragma unroll
-            for (int s = 0; s < S; ++s) {
-              const uint32_t e = decStep<false>(st[c][s], true, lut[s], mask, pb, hv);
-              segLane[c][s][tr * 32] = uint16_t(e >> 16);
-            }
-        }
-      }
-    } else {
-      const int32_t tTop = min(int32_t(T) - 1, g * int32_t(dec::kSegSteps) + int32_t(dec::kSegSteps) - 1);
-      const int32_t tBot = g * int32_t(dec::kSegSteps);
-      for (int32_t t = tTop; t >= tBot; --t) {
-#pragma unroll
-        for (int c = 0; c < K; ++c)
-#pragma unroll
-          for (int s = 0; s < S; ++s) ringEnsure(st[c][s], lane, vecIn);
-#pragma unroll
+    lp<const u32x2> lut[S];
+  #pragma unroll
+    for (int s = 0; s < S; ++s) lut[s] = (lp<const u32x2>)(L + s * (lutBytes / S));
+
+    // segments [0, nFull) are full for every block of the wave; the partial
+    // top segments (element tail / odd block count) are decoded first, masked
+    uint32_t nFull = ~0u;
+  #pragma unroll
+    for (int c = 0; c < K; ++c) nFull = min(nFull, min(uwH[c][0], uwH[c][1]) / dec::kSegWords);
+    const int32_t nSeg = int32_t(divUp(T, dec::kSegSteps));
+    const uint32_t off = 16 * l;  // this lane's chunk in a segment
+
+    // Per segment the VMEM order is: [steps: LDS only] [boundary refill from
+    // the prefetch registers] [join: raw bytes loaded a segment earlier,
+    // 16 B stores] [issue the next segment's raw loads and ring prefetches].
+    // Every s_waitcnt vmcnt then finds only operations issued a whole step
+    // phase earlier.  kVec: 16 B aligned input and output (once per wave).
+    auto run = [&](auto vecTag) {
+      constexpr bool kVec = decltype(vecTag)::value;
+      uint4 rv[K][R];
+      auto i0x = [&](int k) { return uint32_t(k) + lane; };
+      auto loadRaw = [&](int32_t g, bool fullSeg) {
+        const uint32_t segW0 = uint32_t(g) * dec::kSegWords;
+  #pragma unroll
         for (int c = 0; c < K; ++c) {
           const uint32_t uw = lane >= 32 ? uwH[c][1] : uwH[c][0];
-          const bool valid = uint32_t(t) * 32 + l < uw;
-#pragma unroll
-          for (int s = 0; s < S; ++s) {
-            const uint32_t e = decStep<true>(st[c][s], valid, lut[s], mask, pb, hv);
-            if (valid) segLane[c][s][(t - tBot) * 32] = uint16_t(e >> 16);
+          const uint32_t bk = blk0 + 2 * c + (lane >> 5);
+          if (FT != 0 && kVec && (fullSeg || segW0 + off + 16 <= uw)) {
+            if (DG_EXP == 4) {
+  #pragma unroll
+              for (int k = 0; k < R; ++k) rv[c][k] = make_uint4(i0x(k), 0, 0, 0);
+            } else {
+              Join<FT>::load(rv[c], raw, n, bk * kBlockSize + segW0 + off);
+            }
           }
         }
-      }
-    }
-    __builtin_amdgcn_wave_barrier();
-
-    // join + store this segment
-#pragma unroll
-    for (int c = 0; c < K; ++c) {
-      const uint32_t uw = lane >= 32 ? uwH[c][1] : uwH[c][0];
-      const uint32_t bk = blk0 + 2 * c + (lane >> 5);
-      if (segW0 + off >= uw) continue;
-      const uint32_t cnt = min(16u, uw - segW0 - off);
-      const uint32_t i0 = bk * kBlockSize + segW0 + off;
-      lp<const uint16_t> q0 = segLane[c][0] - l + off;
-      lp<const uint16_t> q1 = segLane[c][S - 1] - l + off;
-      if ((FT == 0 || vecIn) && vecOut && cnt == 16) {
-        uint32_t sv[8], sv1[8];
-        const u32x4 a0 = *(lp<const u32x4>)q0, a1 = *(lp<const u32x4>)(q0 + 8);
-        sv[0] = a0.x; sv[1] = a0.y; sv[2] = a0.z; sv[3] = a0.w;
-        sv[4] = a1.x; sv[5] = a1.y; sv[6] = a1.z; sv[7] = a1.w;
-        if constexpr (S == 2) {
-          const u32x4 b0 = *(lp<const u32x4>)q1, b1 = *(lp<const u32x4>)(q1 + 8);
-          sv1[0] = b0.x; sv1[1] = b0.y; sv1[2] = b0.z; sv1[3] = b0.w;
-          sv1[4] = b1.x; sv1[5] = b1.y; sv1[6] = b1.z; sv1[7] = b1.w;
-        } else {
-#pragma unroll
-          for (int k = 0; k < 8; ++k) sv1[k] = 0;
+      };
+      auto join = [&](int32_t g, bool fullSeg) {
+        const uint32_t segW0 = uint32_t(g) * dec::kSegWords;
+  #pragma unroll
+        for (int c = 0; c < K && DG_EXP != 1; ++c) {
+          const uint32_t uw = lane >= 32 ? uwH[c][1] : uwH[c][0];
+          const uint32_t bk = blk0 + 2 * c + (lane >> 5);
+          if (!fullSeg && segW0 + off >= uw) continue;
+          const uint32_t cnt = fullSeg ? 16u : min(16u, uw - segW0 - off);
+          const uint32_t i0 = bk * kBlockSize + segW0 + off;
+          lp<const uint16_t> q0 = segLane[c][0] - l + off;
+          lp<const uint16_t> q1 = segLane[c][S - 1] - l + off;
+          if (kVec && cnt == 16) {
+            uint32_t sv[8], sv1[8];
+            const u32x4 a0 = *(lp<const u32x4>)q0, a1 = *(lp<const u32x4>)(q0 + 8);
+            sv[0] = a0.x; sv[1] = a0.y; sv[2] = a0.z; sv[3] = a0.w;
+            sv[4] = a1.x; sv[5] = a1.y; sv[6] = a1.z; sv[7] = a1.w;
+            if constexpr (S == 2) {
+              const u32x4 b0 = *(lp<const u32x4>)q1, b1 = *(lp<const u32x4>)(q1 + 8);
+              sv1[0] = b0.x; sv1[1] = b0.y; sv1[2] = b0.z; sv1[3] = b0.w;
+              sv1[4] = b1.x; sv1[5] = b1.y; sv1[6] = b1.z; sv1[7] = b1.w;
+            } else {
+  #pragma unroll
+              for (int k = 0; k < 8; ++k) sv1[k] = 0;
+            }
+            Join<FT>::vec(outB, i0, sv, sv1, rv[c]);
+          } else {
+            gp<WordT> o = (gp<WordT>)outB;
+            for (uint32_t k = 0; k < cnt; ++k)
+              o[i0 + k] = Join<FT>::one(q0[k] >> 8, q1[k] >> 8, raw, n, i0 + k);
+          }
         }
-        Join<FT>::vec(outB, i0, sv, sv1, rv[c]);
-      } else {
-        gp<WordT> o = (gp<WordT>)outB;
-        for (uint32_t k = 0; k < cnt; ++k)
-          o[i0 + k] = Join<FT>::one(q0[k] >> 8, q1[k] >> 8, raw, n, i0 + k);
+      };
+      auto boundary = [&]() {
+  #pragma unroll
+        for (int c = 0; c < K; ++c)
+  #pragma unroll
+          for (int s = 0; s < S; ++s) ringRefill<int(dec::kRefill), false>(st[c][s], lane, kVec);
+      };
+      auto reissue = [&]() {
+  #pragma unroll
+        for (int c = 0; c < K; ++c)
+  #pragma unroll
+          for (int s = 0; s < S; ++s)
+  #pragma unroll
+            for (int hh = 0; hh < 2; ++hh) ringPrefetch(st[c][s], hh, lane, kVec);
+      };
+
+      if (nSeg > 0) loadRaw(nSeg - 1, uint32_t(nSeg - 1) < nFull);
+      // partial segments: masked steps
+      for (int32_t g = nSeg - 1; g >= int32_t(nFull); --g) {
+        const int32_t tTop = min(int32_t(T) - 1, g * int32_t(dec::kSegSteps) + int32_t(dec::kSegSteps) - 1);
+        const int32_t tBot = g * int32_t(dec::kSegSteps);
+        for (int32_t t = tTop; t >= tBot; --t) {
+  #pragma unroll
+          for (int c = 0; c < K; ++c)
+  #pragma unroll
+            for (int s = 0; s < S; ++s) ringRefill<32, true>(st[c][s], lane, kVec);
+  #pragma unroll
+          for (int c = 0; c < K; ++c) {
+            const uint32_t uw = lane >= 32 ? uwH[c][1] : uwH[c][0];
+            const bool valid = uint32_t(t) * 32 + l < uw;
+  #pragma unroll
+            for (int s = 0; s < S; ++s) {
+              const uint32_t e = decStep<true>(st[c][s], valid, lut[s], mask, pb, hv);
+              if (valid) segLane[c][s][(t - tBot) * 32] = uint16_t(e >> 16);
+            }
+          }
+        }
+        __builtin_amdgcn_wave_barrier();
+        boundary();
+        join(g, false);
+        __builtin_amdgcn_wave_barrier();
+        if (g > 0) loadRaw(g - 1, uint32_t(g - 1) < nFull);
+        reissue();
       }
-    }
+      // full segments: unrolled, unmasked
+      DG_STAMP(1);
+      for (int32_t g = min(nSeg, int32_t(nFull)) - 1; g >= 0; --g) {
+  #pragma unroll
+        for (int grp = int(dec::kSegSteps / dec::kUnroll) - 1; grp >= 0 && DG_EXP != 6; --grp) {
+  #pragma unroll
+          for (int c = 0; c < K; ++c)
+  #pragma unroll
+            for (int s = 0; s < S; ++s)
+              ringRefill<int(32 * dec::kUnroll), true>(st[c][s], lane, kVec);
+  #pragma unroll
+          for (int u = int(dec::kUnroll) - 1; u >= 0; --u) {
+            const int tr = grp * int(dec::kUnroll) + u;  // step within segment
+  #pragma unroll
+            for (int c = 0; c < K; ++c)
+  #pragma unroll
+              for (int s = 0; s < S; ++s) {
+                const uint32_t e = decStep<false>(st[c][s], true, lut[s], mask, pb, hv);
+                segLane[c][s][tr * 32] = uint16_t(e >> 16);
+              }
+          }
+        }
+        __builtin_amdgcn_wave_barrier();
+        DG_STAMP(2 + 2 * (g & 7));
+        boundary();
+        join(g, true);
+        __builtin_amdgcn_wave_barrier();
+        if (g > 0) loadRaw(g - 1, true);
+        reissue();
+        DG_STAMP(3 + 2 * (g & 7));
+  #if DG_EXP == 7
+        if (g == 0 && lane == 0 && blockIdx.y * gridDim.x * 4 < 16384)
+          g_dbgT[((blockIdx.y * gridDim.x + blockIdx.x) * 4 + w) * 24 + 21] = __builtin_amdgcn_s_memrealtime();
+  #endif
+      }
+    };
+    if (vecIn && vecOut)
+      run(std::true_type{});
+    else
+      run(std::false_type{});
     __builtin_amdgcn_wave_barrier();
   }
 }

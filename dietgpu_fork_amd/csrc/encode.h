@@ -23,16 +23,18 @@ namespace dietgpu {
 constexpr int kThreads = 256;
 constexpr int kWaves = kThreads / 64;
 constexpr uint32_t kSlotBytes = kStateBytesPerBlock + kSlotDataBytes;
-constexpr int kHistCopies = 16;
-constexpr int kHistPitch = kNumSymbols + 1;
 
 // ---------------------------------------------------------------------------
 // k_hist: per-chunk symbol histogram(s) (+ byte-XOR checksum for raw bytes).
 // grid (chunksPerElem, batch).  Each workgroup writes its 256 (x segs)
 // partial counts without atomics; k_normalize sums them.  LDS counters are
-// privatised 16 ways (lane & 15, pitch 257) so the few hot exponent values of
-// float data do not serialise on one LDS address / bank.
+// laid out bin-major with one column per lane of a 32-lane group
+// (hs[sym * 32 + (lane & 31)]): every ds_add of a wave half hits 32
+// distinct banks and never the same address, however skewed the symbol
+// distribution (float exponents concentrate on a handful of values).
 // ---------------------------------------------------------------------------
+constexpr int kHistCols = 32;
+
 template <int FT, bool kChecksum>
 __global__ __launch_bounds__(kThreads) void k_hist(BatchDesc in, uint32_t batchOffset,
                                                    uint32_t numInBatch, uint32_t chunkWords,
@@ -41,24 +43,35 @@ __global__ __launch_bounds__(kThreads) void k_hist(BatchDesc in, uint32_t batchO
                                                    uint32_t* __restrict__ partCk) {
   using WordT = typename FloatTraits<FT>::WordT;
   constexpr int kSegs = FloatTraits<FT>::kSegs;
-  __shared__ uint32_t hs[kSegs][kHistCopies * kHistPitch];
+  __shared__ __attribute__((aligned(16))) uint32_t hs[kSegs][kNumSymbols * kHistCols];
   __shared__ uint32_t red[kWaves];
 
   const uint32_t b = batchOffset + blockIdx.y;
   const uint32_t c = blockIdx.x;
   const uint32_t tid = threadIdx.x;
   for (int s = 0; s < kSegs; ++s)
-    for (uint32_t i = tid; i < kHistCopies * kHistPitch; i += kThreads) hs[s][i] = 0;
+    for (uint32_t i = tid; i < kNumSymbols * kHistCols / 4; i += kThreads)
+      *(lp<u32x4>)&hs[s][4 * i] = u32x4{0, 0, 0, 0};
   __syncthreads();
 
   const uint32_t size = in.size(b);
   const uint64_t begin = uint64_t(c) * chunkWords;
   uint32_t ck = 0;
-  uint32_t* h0 = &hs[0][(tid & (kHistCopies - 1)) * kHistPitch];
-  uint32_t* h1 = &hs[kSegs - 1][(tid & (kHistCopies - 1)) * kHistPitch];
+  uint32_t* h0 = &hs[0][tid & (kHistCols - 1)];
+  uint32_t* h1 = &hs[kSegs - 1][tid & (kHistCols - 1)];
+#ifndef DG_EXP
+#define DG_EXP 0
+#endif
+  uint32_t dummy = 0;
   auto addWord = [&](WordT w) {
-    atomicAdd(&h0[compOf<FT>(w, 0)], 1u);
-    if constexpr (kSegs == 2) atomicAdd(&h1[compOf<FT>(w, 1)], 1u);
+    if (DG_EXP == 8) {
+      h0[compOf<FT>(w, 0) * kHistCols] = tid;  // experiment: plain store
+    } else if (DG_EXP == 9) {
+      dummy += compOf<FT>(w, 0);  // experiment: no LDS
+    } else {
+      atomicAdd(&h0[compOf<FT>(w, 0) * kHistCols], 1u);
+      if constexpr (kSegs == 2) atomicAdd(&h1[compOf<FT>(w, 1) * kHistCols], 1u);
+    }
   };
 
   if (begin < size) {
@@ -76,11 +89,13 @@ __global__ __launch_bounds__(kThreads) void k_hist(BatchDesc in, uint32_t batchO
     }
     gp<const uint4> q4 = (gp<const uint4>)(q + head);
     const uint32_t n4 = (n - head) / kPerVec;
+    // software-pipelined main part: the next 4-vector batch is in flight
+    // while the current one is counted (uniform trip count, so the loads
+    // are unconditional and each wait is a counted vmcnt)
+    constexpr uint32_t kB = 4 * kThreads;
+    const uint32_t nIt = n4 / kB;
     uint32_t i = tid;
-    for (; i + 3 * kThreads < n4; i += 4 * kThreads) {
-      uint4 v[4];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) v[k] = ld16(q4 + i + k * kThreads);
+    auto count4 = [&](const uint4 (&v)[4]) {
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const WordT* ws = reinterpret_cast<const WordT*>(&v[k]);
@@ -88,6 +103,22 @@ __global__ __launch_bounds__(kThreads) void k_hist(BatchDesc in, uint32_t batchO
         for (uint32_t j = 0; j < kPerVec; ++j) addWord(ws[j]);
         if constexpr (kChecksum) ck ^= v[k].x ^ v[k].y ^ v[k].z ^ v[k].w;
       }
+    };
+    if (nIt > 0) {
+      uint4 cur[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) cur[k] = ld16(q4 + i + k * kThreads);
+      for (uint32_t it = 1; it < nIt; ++it) {
+        uint4 nxt[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) nxt[k] = ld16(q4 + i + kB + k * kThreads);
+        count4(cur);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) cur[k] = nxt[k];
+        i += kB;
+      }
+      count4(cur);
+      i += kB;
     }
     for (; i < n4; i += kThreads) {
       const uint4 v = ld16(q4 + i);
@@ -102,11 +133,13 @@ __global__ __launch_bounds__(kThreads) void k_hist(BatchDesc in, uint32_t batchO
       if constexpr (kChecksum) ck ^= uint32_t(w);
     }
   }
+  if (DG_EXP == 9 && dummy == 0x12345678u) hs[0][0] = 1;
   __syncthreads();
   for (int s = 0; s < kSegs; ++s) {
+    // bin tid: sum its 32 columns, rotated so the wave's reads spread banks
     uint32_t sum = 0;
 #pragma unroll
-    for (int k = 0; k < kHistCopies; ++k) sum += hs[s][k * kHistPitch + tid];
+    for (int k = 0; k < kHistCols; ++k) sum += hs[s][tid * kHistCols + ((k + tid) & (kHistCols - 1))];
     G(partHist)[((uint64_t(s) * numInBatch + b) * chunksPerElem + c) * kNumSymbols + tid] = sum;
   }
   if constexpr (kChecksum) {
