@@ -51,6 +51,7 @@ def main():
     import dietgpu_fork_amd  # noqa: F401
     from dietgpu_fork_amd import _native as N
     from dietgpu_fork_amd import codec as C
+    from dietgpu_fork_amd import dist as D
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -77,7 +78,6 @@ def main():
     ok = torch.empty([nb], dtype=torch.uint8, device=dev)
     osz = torch.empty([nb], dtype=torch.int32, device=dev)
     ws = C.Workspace(768 << 20, dev)
-    gathered = torch.empty([nb * world], dtype=torch.int32, device=dev)
 
     in_ptrs = N.ptr_array([x.data_ptr() + i * n * 2 for i in range(nb)])
     in_size = N.u32_array([n] * nb)
@@ -89,8 +89,8 @@ def main():
     def step():
         N.check(L.dietgpu_float_compress(ws.h, ft, pb, 0, nb, in_ptrs, in_size, comp_ptrs,
                                          sizes.data_ptr(), stream))
-        if world > 1:
-            dist.all_gather_into_tensor(gathered, sizes)
+        if world > 1:  # the only exchange: per-element compressed sizes (RCCL)
+            D.gather_sizes(sizes, nb * world)
         N.check(L.dietgpu_float_decompress(ws.h, ft, pb, 0, nb, comp_ptrs, out_ptrs, caps,
                                            ok.data_ptr(), osz.data_ptr(), stream))
 
