@@ -17,6 +17,7 @@ import ctypes
 import glob
 import json
 import os
+import re
 import sys
 import time
 
@@ -178,7 +179,10 @@ def main():
 def _pmc_traffic(kernel, U, comp):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC
     summary (profiles/*pmc*.json, written by tools/pmc_summary.py), or None."""
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")), key=os.path.getmtime)
+    def natural(f):  # r01_v10 after r01_v9
+        return [int(t) if t.isdigit() else t for t in re.split(r"(\d+)", os.path.basename(f))]
+
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")), key=natural)
     for f in reversed(files):  # newest summary first
         try:
             d = json.load(open(f))
