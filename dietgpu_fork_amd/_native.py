@@ -74,6 +74,7 @@ def _declare(L):
         "dietgpu_float_decompress_batch_stride": (c_int, [vp, c_int, c_int, c_int, c_u32, P,
                                                           c_u64, P, c_u64, c_u32, P, P, P]),
         "dietgpu_profile_enable": (None, [c_int]),
+        "dietgpu_profile_filter": (None, [ctypes.c_char_p]),
         "dietgpu_profile_reset": (None, []),
         "dietgpu_profile_query": (c_int, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_double),
                                           ctypes.POINTER(ctypes.c_uint64)]),

@@ -218,6 +218,11 @@ def profile(on=True):
     N.lib().dietgpu_profile_enable(int(on))
 
 
+def profile_filter(family=None):
+    """Record only `family` (None = all families)."""
+    N.lib().dietgpu_profile_filter(family.encode() if family else None)
+
+
 def profile_reset():
     N.lib().dietgpu_profile_reset()
 

@@ -293,6 +293,7 @@ int dietgpu_float_decompress_batch_stride(dietgpu_stack* res, int ft, int pb, in
 }
 
 void dietgpu_profile_enable(int on) { prof::setEnabled(on != 0); }
+void dietgpu_profile_filter(const char* kernel) { prof::setFilter(kernel); }
 void dietgpu_profile_reset(void) { prof::reset(); }
 int dietgpu_profile_query(const char* kernel, double* total_ms, uint64_t* launches) {
   return prof::query(kernel, total_ms, launches) ? DIETGPU_OK : DIETGPU_ERR_INVALID;

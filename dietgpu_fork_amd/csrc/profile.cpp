@@ -18,6 +18,7 @@ struct Family {
 };
 std::atomic<bool> gEnabled{false};
 std::mutex gMu;
+std::string gFilter;  // guarded by gMu
 std::map<std::string, Family>& families() {
   static std::map<std::string, Family> m;
   return m;
@@ -51,6 +52,10 @@ void drain(Family& f) {
 
 bool enabled() { return gEnabled.load(std::memory_order_relaxed); }
 void setEnabled(bool on) { gEnabled.store(on); }
+void setFilter(const char* family) {
+  std::lock_guard<std::mutex> g(gMu);
+  gFilter = family ? family : "";
+}
 
 void reset() {
   std::lock_guard<std::mutex> g(gMu);
@@ -78,6 +83,7 @@ bool query(const char* family, double* totalMs, uint64_t* launches) {
 Scope::Scope(const char* family, hipStream_t s) : family_(family), stream_(s) {
   if (!enabled()) return;
   std::lock_guard<std::mutex> g(gMu);
+  if (!gFilter.empty() && gFilter != family) return;
   start_ = getEvent();
   (void)hipEventRecord(start_, stream_);
 }

@@ -12,6 +12,10 @@ namespace prof {
 
 bool enabled();
 void setEnabled(bool on);
+// Restrict recording to one kernel family (nullptr / "" = all families), so a
+// timed region can price its dominant kernel without an event pair around
+// every launch of the call.
+void setFilter(const char* family);
 void reset();
 // Returns false if the family has never been recorded.
 bool query(const char* family, double* totalMs, uint64_t* launches);

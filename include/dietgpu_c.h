@@ -167,6 +167,8 @@ int dietgpu_float_decompress_batch_stride(dietgpu_stack* res, int float_type, in
  * by hipEvents on its own stream; query returns the summed milliseconds and
  * the launch count since the last reset (synchronises the recorded events). */
 void dietgpu_profile_enable(int on);
+/* record only kernel family `kernel` (NULL or "" = every family) */
+void dietgpu_profile_filter(const char* kernel);
 int dietgpu_profile_query(const char* kernel, double* total_ms, uint64_t* launches);
 void dietgpu_profile_reset(void);
 
