@@ -729,33 +729,64 @@ __global__ __launch_bounds__(kThreads) void k_coalesce(
     }
   }
 
-  // copy this workgroup's blocks: one wave per block
+  // per block: states (32 lanes) and the blockWords entry
   const uint32_t lane = tid & 63;
+  __shared__ uint32_t cwL[kThreads];
+  cwL[tid] = cwj;
   for (uint32_t k = first + (tid >> 6); k < last; k += kWaves) {
-    const uint32_t c = cwS[k];
-    const uint32_t p = pre[k - first];
     gp<const uint8_t> slot = G(slots) + ((uint64_t(seg) * numInBatch + b) * MB + k) * kSlotBytes;
-    if (lane < 32) {
+    if (lane < 32)
       ((gp<uint32_t>)(states + uint64_t(kStateBytesPerBlock) * k))[lane] = ((gp<const uint32_t>)slot)[lane];
-    }
-    if (lane == 0) {
+    if (lane == 32) {
       const uint32_t uwk = (k + 1 < nBlocks || n % kBlockSize == 0) ? kBlockSize : n % kBlockSize;
-      st8(bwords + k, make_uint2((uwk << 16) | c, p));
+      st8(bwords + k, make_uint2((uwk << 16) | cwS[k], pre[k - first]));
     }
-    gp<const uint4> src = (gp<const uint4>)(slot + kStateBytesPerBlock);
-    gp<uint4> dst = (gp<uint4>)(data + 2ull * p);
-    const uint32_t nv = divUp(c, 8);
-    for (uint32_t i = lane; i < nv; i += 64) {
-      uint4 v = ld16(src + i);
-      const uint32_t valid = c - i * 8;
-      if (valid < 8) {
-        uint32_t* vw = reinterpret_cast<uint32_t*>(&v);
+  }
+  __syncthreads();
+  // payload: the workgroup's blocks are contiguous in the archive, so every
+  // thread copies 16 B vectors (8 words) across the whole range, the source
+  // block found by binary search over the LDS prefix; 4 vectors in flight
+  // per thread.  Words past a block's count are written as 0.
+  const uint32_t nk = last > first ? last - first : 0;
+  if (nk == 0) return;
+  const uint32_t w0 = pre[0];
+  const uint32_t nv = (pre[nk - 1] + roundUp(cwL[nk - 1], 8) - w0) / 8;
+  gp<uint4> dst = (gp<uint4>)(data + 2ull * w0);
+  gp<const uint8_t> slot0 = G(slots) + ((uint64_t(seg) * numInBatch + b) * MB + first) * kSlotBytes +
+                            kStateBytesPerBlock;
+  constexpr int kIn = 4;
+  for (uint32_t v0 = tid; v0 < nv; v0 += kIn * kThreads) {
+    uint4 val[kIn];
+    uint32_t valid[kIn];
 #pragma unroll
-        for (uint32_t q = 0; q < 4; ++q) {
-          if (2 * q + 1 >= valid) vw[q] &= (2 * q < valid) ? 0xffffu : 0u;
+    for (int q = 0; q < kIn; ++q) {
+      const uint32_t v = v0 + q * kThreads;
+      valid[q] = 0;
+      if (v < nv) {
+        const uint32_t w = w0 + 8 * v;
+        uint32_t lo = 0, hi = nk;  // last k with pre[k] <= w
+        while (hi - lo > 1) {
+          const uint32_t mid = (lo + hi) >> 1;
+          if (pre[mid] <= w) lo = mid; else hi = mid;
+        }
+        const uint32_t off = w - pre[lo];
+        valid[q] = cwL[lo] > off ? cwL[lo] - off : 0;
+        val[q] = ld16((gp<const uint4>)(slot0 + uint64_t(lo) * kSlotBytes + 2ull * off));
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < kIn; ++q) {
+      const uint32_t v = v0 + q * kThreads;
+      if (v >= nv) continue;
+      uint4 x = val[q];
+      if (valid[q] < 8) {
+        uint32_t* vw = reinterpret_cast<uint32_t*>(&x);
+#pragma unroll
+        for (uint32_t r = 0; r < 4; ++r) {
+          if (2 * r + 1 >= valid[q]) vw[r] &= (2 * r < valid[q]) ? 0xffffu : 0u;
         }
       }
-      st16(dst + i, v);
+      st16(dst + v, x);
     }
   }
 }
