@@ -158,6 +158,47 @@ __device__ __forceinline__ uint32_t decStep(DStream& p, bool valid, lp<const u32
   return e.x;
 }
 
+// All chains of a wave, one step each, in three phases separated by
+// scheduling barriers: (A) every chain's table read, (B) every chain's state
+// update, ballot and ring read, (C) every chain's v_perm.  Without the
+// barriers the scheduler serialises the chains (one LDS round trip exposed
+// per chain-step); with them the LDS latencies of the chains overlap.
+// Returns the table entries' low words (sym in bits 24-31) in e0[].
+template <bool kMask, int NC>
+__device__ __forceinline__ void decStepAll(DStream* const (&p)[NC], const bool (&valid)[NC],
+                                           lp<const u32x2> const (&lut)[NC], uint32_t mask, int pb,
+                                           uint32_t hv, uint32_t (&e0)[NC]) {
+  u32x2 e[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) e[c] = lut[c][p[c]->x & mask];
+  __builtin_amdgcn_sched_barrier(0);
+  uint32_t xn[NC], v[NC];
+  bool rd[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    DStream& q = *p[c];
+    xn[c] = __umul24(e[c].x, q.x >> pb) + e[c].y;
+    if (kMask) xn[c] = valid[c] ? xn[c] : q.x;
+    rd[c] = kMask ? (valid[c] && xn[c] < kMinState) : (xn[c] < kMinState);
+    const uint64_t vote = ballot(rd[c]);
+    const int32_t cLo = __popc(uint32_t(vote));
+    const int32_t cHi = __popc(uint32_t(vote >> 32));
+    const int32_t baseLo = q.ptr[0] - cLo;
+    const int32_t diff = q.ptr[1] - q.ptr[0] - cHi;
+    q.ptr[0] = baseLo;
+    q.ptr[1] -= cHi;
+    const uint32_t vbase = uint32_t(baseLo) + (hv & uint32_t(diff));
+    const uint32_t idx = __builtin_amdgcn_mbcnt_hi(uint32_t(vote >> 32),
+                                                   __builtin_amdgcn_mbcnt_lo(uint32_t(vote), vbase));
+    v[c] = q.ringLane[idx & (dec::kRing - 1)];
+    e0[c] = e[c].x;
+  }
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int c = 0; c < NC; ++c)
+    p[c]->x = __builtin_amdgcn_perm(xn[c], v[c], rd[c] ? 0x05040100u : 0x07060504u);
+}
+
 // Join 8 decoded symbols (u16 sym << 8 in LDS) with their raw bytes.
 template <int FT>
 struct Join {
@@ -418,6 +459,18 @@ __global__ __launch_bounds__(dec::kThreads) void k_decode(BatchDesc in, BatchDes
     const int32_t nSeg = int32_t(divUp(T, dec::kSegSteps));
     const uint32_t off = dec::kChunk * l;  // this lane's chunk in a segment
 
+    DStream* chains[K * S];
+    lp<const u32x2> lutC[K * S];
+    bool allValid[K * S];
+#pragma unroll
+    for (int c = 0; c < K; ++c)
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        chains[c * S + s] = &st[c][s];
+        lutC[c * S + s] = lut[s];
+        allValid[c * S + s] = true;
+      }
+
     // kVec: 16 B aligned input and output (once per wave): full segments
     // then load and join unconditionally.
     auto run = [&](auto vecTag) {
@@ -474,16 +527,20 @@ __global__ __launch_bounds__(dec::kThreads) void k_decode(BatchDesc in, BatchDes
           for (int c = 0; c < K; ++c)
 #pragma unroll
             for (int s = 0; s < S; ++s) ringEnsure(st[c][s], lane, kVec);
+          bool vld[K * S];
 #pragma unroll
           for (int c = 0; c < K; ++c) {
             const uint32_t uw = lane >= 32 ? uwH[c][1] : uwH[c][0];
-            const bool valid = uint32_t(t) * 32 + l < uw;
 #pragma unroll
-            for (int s = 0; s < S; ++s) {
-              const uint32_t e = decStep<true>(st[c][s], valid, lut[s], mask, pb, hv);
-              if (valid) segLane[c][s][(t - tBot) * 32] = uint16_t(e >> 16);
-            }
+            for (int s = 0; s < S; ++s) vld[c * S + s] = uint32_t(t) * 32 + l < uw;
           }
+          uint32_t e0[K * S];
+          decStepAll<true, K * S>(chains, vld, lutC, mask, pb, hv, e0);
+#pragma unroll
+          for (int c = 0; c < K; ++c)
+#pragma unroll
+            for (int s = 0; s < S; ++s)
+              if (vld[c * S + s]) segLane[c][s][(t - tBot) * 32] = uint16_t(e0[c * S + s] >> 16);
         }
         __builtin_amdgcn_wave_barrier();
         join(g, false);
@@ -502,13 +559,12 @@ __global__ __launch_bounds__(dec::kThreads) void k_decode(BatchDesc in, BatchDes
 #pragma unroll
           for (int u = int(dec::kUnroll) - 1; u >= 0; --u) {
             const int tr = grp * int(dec::kUnroll) + u;  // step within segment
+            uint32_t e0[K * S];
+            decStepAll<false, K * S>(chains, allValid, lutC, mask, pb, hv, e0);
 #pragma unroll
             for (int c = 0; c < K; ++c)
 #pragma unroll
-              for (int s = 0; s < S; ++s) {
-                const uint32_t e = decStep<false>(st[c][s], true, lut[s], mask, pb, hv);
-                segLane[c][s][tr * 32] = uint16_t(e >> 16);
-              }
+              for (int s = 0; s < S; ++s) segLane[c][s][tr * 32] = uint16_t(e0[c * S + s] >> 16);
           }
         }
         __builtin_amdgcn_wave_barrier();

@@ -1,6 +1,6 @@
-"""Experiment 7 analysis (GPU box): per-wave s_memtime phase stamps of
-k_decode (make exp EXP=7).  Runs the c2 bf16 workload once and prints
-per-phase cycle statistics.  Dev tool, not part of the product."""
+"""Experiment 7 analysis (GPU box): per-wave stamps of k_decode (make exp
+EXP=7): s_memrealtime at start (slot 22) / end (slot 21), s_memtime after the
+steps of each full segment (slots 2 + g).  Dev tool, not part of the product."""
 import ctypes
 import os
 import sys
@@ -40,51 +40,21 @@ assert torch.equal(out.view(torch.int16), x.view(torch.int16))
 buf = np.zeros(16384 * 24, dtype=np.uint64)
 L.dietgpu_debug_read.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
 assert L.dietgpu_debug_read(buf.ctypes.data, buf.nbytes) == 0
-T = buf.reshape(16384, 24)[:8192].astype(np.int64)
-T = T[T[:, 0] > 0]
-t0 = T[:, 0].min()
-start, loop = T[:, 0] - t0, T[:, 1] - t0
-print("waves", len(T), "kernel span (cyc)", (T[:, 3] - t0).max())
-print("setup (start->loop): median %d p90 %d" % (np.median(loop - start), np.percentile(loop - start, 90)))
-prev = T[:, 1]
-steps, joins = [], []
-for gseg in range(7, -1, -1):
-    a, b_ = T[:, 2 + 2 * gseg], T[:, 3 + 2 * gseg]
-    steps.append(a - prev)
-    joins.append(b_ - a)
-    prev = b_
-steps, joins = np.array(steps), np.array(joins)
-print("steps per segment: median", np.median(steps, axis=1).astype(int))
-print("join per segment:  median", np.median(joins, axis=1).astype(int), "p90", np.percentile(joins, 90, axis=1).astype(int))
-life = T[:, 3] - T[:, 0]
-print("wave life median %d, p10 %d p90 %d" % (np.median(life), np.percentile(life, 10), np.percentile(life, 90)))
-print("start times histogram (cycles):", np.histogram(start, bins=8)[0], np.histogram(start, bins=8)[1].astype(int))
-hw = T[:, 23] & 0xffffffff
-simd = (hw >> 4) & 3
-cu = (hw >> 8) & 15
-se = (hw >> 13) & 7
-xcc = (T[:, 23] >> 32) & 0xf
-print("distinct (xcc,se,cu,simd):", len(set(zip(xcc, se, cu, simd))))
-rt = (T[:, 21] - T[:, 22]).astype(np.float64) / 100e6  # s_memrealtime: 100 MHz
-cyc = (T[:, 3] - T[:, 0]).astype(np.float64)
-print("shader clock estimate (GHz): median %.3f" % np.median(cyc / rt / 1e9))
-for xc in sorted(set(xcc.tolist()))[:2]:
-    m = xcc == xc
-    st = np.sort(T[m, 0] - T[m, 0].min())
-    print("xcc", xc, "waves", m.sum(), "start quantiles (cyc):", np.percentile(st, [0, 25, 50, 60, 75, 100]).astype(int),
-          "end max", int((T[m, 3] - T[m, 0].min()).max()))
-# concurrency from the chip-wide 100 MHz clock
+T = buf.reshape(16384, 24).astype(np.int64)
+T = T[T[:, 22] > 0]
 s_rt, e_rt = T[:, 22], T[:, 21]
 base = s_rt.min()
-print("realtime span (us): %.1f" % ((e_rt.max() - base) / 100.0))
-grid = np.arange(0, e_rt.max() - base + 1, 50)  # 0.5 us steps
+life = (e_rt - s_rt) / 100.0
+print("waves", len(T), "span (us) %.1f" % ((e_rt.max() - base) / 100.0))
+print("wave life (us) quantiles 0/10/50/90/100:", np.percentile(life, [0, 10, 50, 90, 100]).round(1).tolist())
+print("wave start (us) quantiles:", np.percentile((s_rt - base) / 100.0, [0, 50, 100]).round(1).tolist())
+grid = np.arange(0, e_rt.max() - base + 1, 50)
 live = np.array([((s_rt - base <= t) & (e_rt - base > t)).sum() for t in grid])
-print("live waves over time (every 5 us):", live[::10].tolist())
-print("wave start (us) quantiles:", np.percentile((s_rt - base) / 100.0, [0, 10, 25, 50, 75, 90, 100]).round(1).tolist())
-print("wave life (us) quantiles:", np.percentile((e_rt - s_rt) / 100.0, [0, 10, 50, 90, 100]).round(1).tolist())
-life_us = (e_rt - s_rt) / 100.0
-for name, key in (("xcc", xcc), ("simd", simd), ("se", se)):
-    print("life by", name, {int(k): round(float(life_us[key == k].mean()), 1) for k in sorted(set(key.tolist()))})
-wv = np.arange(len(T))
-print("life by wave-in-WG", {k: round(float(life_us[(wv % 4) == k].mean()), 1) for k in range(4)})
-print("life by tensor parity (blockIdx.x)", {k: round(float(life_us[((wv // 4) % 4) == k].mean()), 1) for k in range(4)})
+print("live waves every 5 us:", live[::10].tolist())
+# per-segment cycles: stamps after steps of segment g (descending g)
+seg = T[:, 2:18]
+d = -np.diff(seg[:, ::-1], axis=1)  # g=15..0 order reversed: time between consecutive segments
+steps_plus_join = np.diff(seg[:, ::-1][:, ::-1], axis=1)
+print("cycles between consecutive segment stamps (median, g=15->0):",
+      np.median(-np.diff(seg, axis=1)[:, ::-1], axis=0).astype(int).tolist())
+print("loop start -> first stamp median:", int(np.median(seg[:, 15] - T[:, 1])))
