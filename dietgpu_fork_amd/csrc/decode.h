@@ -115,6 +115,7 @@ __device__ __forceinline__ void ringPrefetch(DStream& p, int hh, uint32_t lane, 
 // overwrites words >= lo + 128, all consumed since ptr < lo + 128) and
 // prefetch the next 128 words.
 __device__ __forceinline__ void ringEnsure(DStream& p, uint32_t lane, bool vec) {
+  if (DG_EXP == 3 || DG_EXP == 15) return;  // experiment: no refills
 #pragma unroll
   for (int hh = 0; hh < 2; ++hh) {
     if (p.lo[hh] > 0 && p.ptr[hh] - int32_t(32 * dec::kUnroll) < p.lo[hh]) {
@@ -475,8 +476,10 @@ __global__ __launch_bounds__(dec::kThreads) void k_decode(BatchDesc in, BatchDes
     // then load and join unconditionally.
     auto run = [&](auto vecTag) {
       constexpr bool kVec = decltype(vecTag)::value;
-      uint32_t rv[K][R];
-      auto loadRaw = [&](int32_t g, bool fullSeg) {
+      // raw float bytes, double-buffered: a full segment's bytes are loaded
+      // before the previous segment's steps, a whole segment ahead of use
+      uint32_t rvA[K][R], rvB[K][R];
+      auto loadRaw = [&](int32_t g, bool fullSeg, uint32_t (&rv)[K][R]) {
         const uint32_t segW0 = uint32_t(g) * dec::kSegWords;
 #pragma unroll
         for (int c = 0; c < K; ++c) {
@@ -486,10 +489,10 @@ __global__ __launch_bounds__(dec::kThreads) void k_decode(BatchDesc in, BatchDes
             Join<FT>::load(rv[c], raw, n, bk * kBlockSize + segW0 + off);
         }
       };
-      auto join = [&](int32_t g, bool fullSeg) {
+      auto join = [&](int32_t g, bool fullSeg, const uint32_t (&rv)[K][R]) {
         const uint32_t segW0 = uint32_t(g) * dec::kSegWords;
 #pragma unroll
-        for (int c = 0; c < K && DG_EXP != 1; ++c) {
+        for (int c = 0; c < K && DG_EXP != 1 && DG_EXP != 15; ++c) {
           const uint32_t uw = lane >= 32 ? uwH[c][1] : uwH[c][0];
           const uint32_t bk = blk0 + 2 * c + (lane >> 5);
           if (!fullSeg && segW0 + off >= uw) continue;
@@ -517,7 +520,7 @@ __global__ __launch_bounds__(dec::kThreads) void k_decode(BatchDesc in, BatchDes
         }
       };
 
-      if (nSeg > 0) loadRaw(nSeg - 1, uint32_t(nSeg - 1) < nFull);
+      if (nSeg > 0) loadRaw(nSeg - 1, uint32_t(nSeg - 1) < nFull, rvA);
       // partial segments: masked steps
       for (int32_t g = nSeg - 1; g >= int32_t(nFull); --g) {
         const int32_t tTop = min(int32_t(T) - 1, g * int32_t(dec::kSegSteps) + int32_t(dec::kSegSteps) - 1);
@@ -543,13 +546,14 @@ __global__ __launch_bounds__(dec::kThreads) void k_decode(BatchDesc in, BatchDes
               if (vld[c * S + s]) segLane[c][s][(t - tBot) * 32] = uint16_t(e0[c * S + s] >> 16);
         }
         __builtin_amdgcn_wave_barrier();
-        join(g, false);
+        join(g, false, rvA);
         __builtin_amdgcn_wave_barrier();
-        if (g > 0) loadRaw(g - 1, uint32_t(g - 1) < nFull);
+        if (g > 0) loadRaw(g - 1, uint32_t(g - 1) < nFull, rvA);
       }
       // full segments: unrolled, unmasked
       DG_STAMP(1);
-      for (int32_t g = min(nSeg, int32_t(nFull)) - 1; g >= 0; --g) {
+      auto fullSeg = [&](int32_t g, const uint32_t (&cur)[K][R], uint32_t (&nxt)[K][R]) {
+        if (g > 0) loadRaw(g - 1, true, nxt);
 #pragma unroll
         for (int grp = int(dec::kSegSteps / dec::kUnroll) - 1; grp >= 0; --grp) {
 #pragma unroll
@@ -569,10 +573,15 @@ __global__ __launch_bounds__(dec::kThreads) void k_decode(BatchDesc in, BatchDes
         }
         __builtin_amdgcn_wave_barrier();
         DG_STAMP(2 + (g & 15));
-        join(g, true);
+        join(g, true, cur);
         __builtin_amdgcn_wave_barrier();
-        if (g > 0) loadRaw(g - 1, true);
+      };
+      int32_t g = min(nSeg, int32_t(nFull)) - 1;  // rvA holds segment g's bytes
+      for (; g >= 1; g -= 2) {
+        fullSeg(g, rvA, rvB);
+        fullSeg(g - 1, rvB, rvA);
       }
+      if (g == 0) fullSeg(0, rvA, rvB);
     };
     if (vecIn && vecOut)
       run(std::true_type{});
