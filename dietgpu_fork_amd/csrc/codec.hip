@@ -6,7 +6,7 @@
 //
 // Launch sequence per call (all stream-ordered, no host sync unless a
 // checksum has to be verified):
-//   compress:   k_hist -> k_normalize -> k_encode -> k_coalesce
+//   compress:   k_hist -> k_normalize -> k_encode (+ k_coalesce for fp64)
 //   decompress: k_decode (table build + rANS decode + float join fused)
 #include <algorithm>
 #include <cstring>
@@ -57,6 +57,7 @@ void encodeBatchDevice(StackDeviceMemory& res, int pb, bool useChecksum, uint32_
   checkProbBits(pb);
   if (nb == 0) return;
   constexpr int kSegs = FloatTraits<FT>::kSegs;
+  constexpr bool kFused = kSegs == 1;  // k_encode writes the archive itself
   const uint32_t MB = divUp(maxSize, kBlockSize);
   const uint32_t chunkWords = histChunkWords(nb, maxSize);
   const uint32_t chunks = std::max(1u, divUp(maxSize, chunkWords));
@@ -70,7 +71,9 @@ void encodeBatchDevice(StackDeviceMemory& res, int pb, bool useChecksum, uint32_
   auto table = res.alloc<uint4>(s, size_t(kSegs) * nb * kNumSymbols);
   auto pdf = res.alloc<uint16_t>(s, size_t(kSegs) * nb * kNumSymbols);
   auto slots = res.alloc<uint8_t>(s, size_t(kSegs) * nb * std::max(MB, 1u) * kSlotBytes);
-  auto cw = res.alloc<uint32_t>(s, size_t(kSegs) * nb * std::max(MB, 1u));
+  auto cw = res.alloc<uint32_t>(s, kFused ? 1 : size_t(kSegs) * nb * std::max(MB, 1u));
+  const uint32_t nW = std::max(1u, divUp(MB, EncCfg<FT>::kBlocksPerWG));
+  auto flags = res.alloc<uint64_t>(s, kFused ? size_t(nb) * nW : 1);
 
   if (FT != 0 && useChecksum) {
     HIP_CHECK(hipMemsetAsync(ck.data(), 0, sizeof(uint32_t) * nb, s));
@@ -102,17 +105,19 @@ void encodeBatchDevice(StackDeviceMemory& res, int pb, bool useChecksum, uint32_
       dim3 g(ny, kSegs);
       k_normalize<<<g, kThreads, 0, s>>>(in, y0, nb, userHist ? hist_dev : partHist.data(),
                                          userHist ? 1u : chunks, pb, table.data(), pdf.data(),
-                                         rawCk ? partCk.data() : nullptr, ck.data());
+                                         rawCk ? partCk.data() : nullptr, ck.data(),
+                                         kFused ? flags.data() : nullptr, nW);
       HIP_LAUNCH_CHECK();
     }
-    if (MB > 0) {
+    if (MB > 0 || kFused) {
       prof::Scope p("encode", s);
-      dim3 g(divUp(MB, EncCfg<FT>::kBlocksPerWG), ny);
-      k_encode<FT><<<g, enc::kThreads, 0, s>>>(in, out, y0, nb, MB, table.data(), slots.data(),
-                                          cw.data());
+      dim3 g(nW, ny);
+      const EncTail tail{pdf.data(), ck.data(), outSize_dev, flags.data(), nW, pb, useChecksum};
+      k_encode<FT><<<g, enc::kThreads, 0, s>>>(in, out, y0, nb, std::max(MB, 1u), table.data(),
+                                               slots.data(), cw.data(), tail);
       HIP_LAUNCH_CHECK();
     }
-    {
+    if (!kFused) {
       prof::Scope p("coalesce", s);
       const uint32_t bpw = 32;
       dim3 g(std::max(1u, divUp(MB, bpw)), ny, kSegs);

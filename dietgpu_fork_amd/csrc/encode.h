@@ -166,13 +166,16 @@ __global__ __launch_bounds__(kThreads) void k_hist(BatchDesc in, uint32_t batchO
 static __global__ __launch_bounds__(kThreads) void k_normalize(
     BatchDesc in, uint32_t batchOffset, uint32_t numInBatch, const uint32_t* __restrict__ hist,
     uint32_t chunksPerElem, int pb, uint4* __restrict__ table, uint16_t* __restrict__ pdfOut,
-    const uint32_t* __restrict__ partCk, uint32_t* __restrict__ ckOut) {
+    const uint32_t* __restrict__ partCk, uint32_t* __restrict__ ckOut, uint64_t* __restrict__ flags,
+    uint32_t nW) {
   __shared__ uint32_t keys[kNumSymbols];
   __shared__ uint32_t red[kWaves];
   const uint32_t b = batchOffset + blockIdx.x;
   const uint32_t seg = blockIdx.y;
   const uint32_t s = threadIdx.x;
   const uint64_t row = uint64_t(seg) * numInBatch + b;
+  if (flags && seg == 0)  // k_encode's look-back flags (EncTail)
+    for (uint32_t i = s; i < nW; i += kThreads) G(flags)[uint64_t(b) * nW + i] = 0;
 
   if (partCk && seg == 0 && s == 0) {
     uint32_t ck = 0;
@@ -368,12 +371,12 @@ __device__ __forceinline__ void splitVec(const uint4& v, uint32_t i0, uint32_t n
     uint32_t r[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) r[k] = rotl32(ws[k], 1);
-    *(lp<uint32_t>)sym0 = __builtin_amdgcn_perm(r[1], r[0], 0x07030703u) & 0xffffu |
+    *(lp<uint32_t>)sym0 = (__builtin_amdgcn_perm(r[1], r[0], 0x07030703u) & 0xffffu) |
                           (__builtin_amdgcn_perm(r[3], r[2], 0x07030703u) << 16);
     st8(raw + 2 * i0, make_uint2(__builtin_amdgcn_perm(r[1], r[0], 0x05040100u),
                                  __builtin_amdgcn_perm(r[3], r[2], 0x05040100u)));
     *(gp<uint32_t>)(raw + 2 * roundUp(n, 8) + i0) =
-        __builtin_amdgcn_perm(r[1], r[0], 0x06020602u) & 0xffffu |
+        (__builtin_amdgcn_perm(r[1], r[0], 0x06020602u) & 0xffffu) |
         (__builtin_amdgcn_perm(r[3], r[2], 0x06020602u) << 16);
   } else {
     const uint64_t r0 = rotl64(ws[0], 1), r1 = rotl64(ws[1], 1);
@@ -411,15 +414,183 @@ __device__ __forceinline__ void splitOne(typename FloatTraits<FT>::WordT w, uint
   }
 }
 
-// grid (ceil(MB / kBlocksPerWG), batch).  Writes per block: slot states,
-// slot words and cw[] (word count).
+// Payload copy of a run of nk consecutive blocks: the blocks are contiguous
+// in the archive (block k at word pre[k], pre in LDS; cwL[k] words), so
+// every thread copies 16 B vectors (8 words) across the whole range, the
+// source slot found by binary search over pre; 4 vectors in flight per
+// thread.  Words past a block's count are written as 0.
+__device__ __forceinline__ void copyPayload(const uint32_t* pre, const uint32_t* cwL, uint32_t nk,
+                                            gp<const uint8_t> slot0, gp<uint8_t> data) {
+  if (nk == 0) return;
+  const uint32_t tid = threadIdx.x;
+  const uint32_t w0 = pre[0];
+  const uint32_t nv = (pre[nk - 1] + roundUp(cwL[nk - 1], 8) - w0) / 8;
+  gp<uint4> dst = (gp<uint4>)(data + 2ull * w0);
+  constexpr int kIn = 4;
+  for (uint32_t v0 = tid; v0 < nv; v0 += kIn * kThreads) {
+    uint4 val[kIn];
+    uint32_t valid[kIn];
+#pragma unroll
+    for (int q = 0; q < kIn; ++q) {
+      const uint32_t v = v0 + q * kThreads;
+      valid[q] = 0;
+      if (v < nv) {
+        const uint32_t w = w0 + 8 * v;
+        uint32_t lo = 0, hi = nk;  // last k with pre[k] <= w
+        while (hi - lo > 1) {
+          const uint32_t mid = (lo + hi) >> 1;
+          if (pre[mid] <= w) lo = mid; else hi = mid;
+        }
+        const uint32_t off = w - pre[lo];
+        valid[q] = cwL[lo] > off ? cwL[lo] - off : 0;
+        val[q] = ld16((gp<const uint4>)(slot0 + uint64_t(lo) * kSlotBytes + 2ull * off));
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < kIn; ++q) {
+      const uint32_t v = v0 + q * kThreads;
+      if (v >= nv) continue;
+      uint4 x = val[q];
+      if (valid[q] < 8) {
+        uint32_t* vw = reinterpret_cast<uint32_t*>(&x);
+#pragma unroll
+        for (uint32_t r = 0; r < 4; ++r) {
+          if (2 * r + 1 >= valid[q]) vw[r] &= (2 * r < valid[q]) ? 0xffffu : 0u;
+        }
+      }
+      st16(dst + v, x);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Fused coalesce (single-segment formats).  Each encode workgroup publishes
+// its blocks' word total and finds its archive offset by a decoupled
+// look-back over the element's earlier workgroups (lower blockIdx.x, so
+// dispatched earlier: waiting on them cannot deadlock), then writes its own
+// blocks' blockWords and payload.  One 8 B flag per (element, workgroup),
+// zeroed by k_normalize: bits 63:62 = 1 aggregate / 2 inclusive prefix, low
+// 32 bits the value.  The value lives in the flag word itself, so a relaxed
+// agent-scope 8 B store/load (sc1: written through, read past L1) is the
+// whole hand-off.
+// ---------------------------------------------------------------------------
+struct EncTail {
+  const uint16_t* pdf;  // normalised pdf rows (k_normalize)
+  const uint32_t* ck;   // per-element checksum (k_normalize / k_checksum)
+  uint32_t* outSize;
+  uint64_t* flags;      // nW per element
+  uint32_t nW;
+  int pb;
+  bool useChecksum;
+};
+
+constexpr uint64_t kFlagAgg = 1ull << 62;
+constexpr uint64_t kFlagPrefix = 2ull << 62;
+
+// Called by one whole wave; returns (wave-uniform) the sum of the values of
+// workgroups [0, x) of the element.
+__device__ __forceinline__ uint32_t lookBack(gp<uint64_t> f, uint32_t x, uint32_t agg) {
+  const uint32_t lane = laneId();
+  if (lane == 0)
+    __hip_atomic_store((uint64_t*)f + x, (x == 0 ? kFlagPrefix : kFlagAgg) | agg, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  if (x == 0) return 0;
+  uint32_t excl = 0;
+  int32_t j = int32_t(x);
+  // predecessors are resident or done, so the wait is short; the cap only
+  // turns a logic error into a wrong archive instead of a hung device
+  for (uint32_t spins = 0; spins < (1u << 24);) {
+    const int32_t k = j - 1 - int32_t(lane);
+    const uint64_t v = k >= 0 ? __hip_atomic_load((uint64_t*)f + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                              : kFlagPrefix;
+    const uint64_t isPre = ballot((v >> 63) != 0);
+    const uint64_t isZero = ballot((v >> 62) == 0);
+    const uint32_t firstPre = isPre ? uint32_t(__builtin_ctzll(isPre)) : 64u;
+    const uint64_t need = firstPre >= 63 ? ~0ull : (2ull << firstPre) - 1;
+    if (isZero & need) {
+      __builtin_amdgcn_s_sleep(2);
+      ++spins;
+      continue;
+    }
+    excl += waveSum(lane <= firstPre ? uint32_t(v) : 0u);
+    if (firstPre < 64) break;
+    j -= 64;
+  }
+  if (lane == 0)
+    __hip_atomic_store((uint64_t*)f + x, kFlagPrefix | uint64_t(excl + agg), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  return excl;
+}
+
+// Header fields known before encoding (all but the word totals): ANS header
+// words 0-2 and 4-7, the pdf table, float header words 0-3 and 5-7, and the
+// raw section's rounding tails.  Whole workgroup.
+template <int FT>
+__device__ void writeHeadFixed(gp<uint8_t> base, gp<uint8_t> o, uint32_t n, uint32_t nBlocks,
+                               const EncTail& t, uint32_t b) {
+  const uint32_t tid = threadIdx.x;
+  const bool ansCk = FT == 0 && t.useChecksum;
+  if (tid == 0) {
+    gp<uint32_t> hdr = (gp<uint32_t>)o;
+    hdr[0] = kANSMagicVersion;
+    hdr[1] = nBlocks;
+    hdr[2] = n;
+    hdr[4] = uint32_t(t.pb) | (ansCk ? 0x10u : 0u);
+    hdr[5] = ansCk ? G(t.ck)[b] : 0u;
+    hdr[6] = 0;
+    hdr[7] = 0;
+    if constexpr (FT != 0) {
+      gp<uint32_t> fh = (gp<uint32_t>)base;
+      fh[0] = kFloatMagicVersion;
+      fh[1] = n;
+      fh[2] = uint32_t(FT) | (t.useChecksum ? 0x10u : 0u);
+      fh[3] = t.useChecksum ? G(t.ck)[b] : 0u;
+      fh[5] = 0;
+      fh[6] = 0;
+      fh[7] = 0;
+    }
+  }
+  ((gp<uint16_t>)(o + kANSHeaderBytes))[tid] = G(t.pdf)[uint64_t(b) * kNumSymbols + tid];
+  if constexpr (FT != 0) {
+    if (tid < 16) {
+      gp<uint8_t> raw = base + 32;
+      if constexpr (FT == 1 || FT == 2) {
+        if (n + tid < roundUp(n, 16)) raw[n + tid] = 0;
+      } else {
+        static_assert(FT == 3, "single-segment float formats only");
+        if (n + tid < roundUp(n, 8)) ((gp<uint16_t>)raw)[n + tid] = 0;
+        if (n + tid < roundUp(n, 16)) raw[2 * roundUp(n, 8) + n + tid] = 0;
+      }
+    }
+  }
+}
+
+// The fields that need the element's word total (last workgroup, one lane).
+template <int FT>
+__device__ void writeHeadTotal(gp<uint8_t> base, gp<uint8_t> o, uint32_t n, uint32_t nBlocks,
+                               uint32_t totalWords, gp<uint2> bwords, const EncTail& t, uint32_t b) {
+  ((gp<uint32_t>)o)[3] = totalWords;
+  if (nBlocks & 1) st8(bwords + nBlocks, make_uint2(0, 0));
+  const uint64_t ansBytes = ansOverhead(nBlocks) + 2ull * totalWords;
+  uint64_t sz = ansBytes;
+  if constexpr (FT != 0) {
+    ((gp<uint32_t>)base)[4] = uint32_t(roundUp64(ansBytes, 16));  // GpuFloatHeader2
+    sz += 32ull + floatRawBytes(FT, n);
+  }
+  if (t.outSize) G(t.outSize)[b] = uint32_t(sz);
+}
+
+// grid (max(1, ceil(MB / kBlocksPerWG)), batch).  Single-segment formats
+// (kFused): writes the whole archive (states straight to it, words via the
+// slots, see EncTail).  fp64: writes per block slot states, slot words and
+// cw[] (word count) for k_coalesce.
 template <int FT>
 __global__ __launch_bounds__(enc::kThreads) void k_encode(BatchDesc in, BatchDesc out,
                                                           uint32_t batchOffset,
                                                           uint32_t numInBatch, uint32_t MB,
                                                           const uint4* __restrict__ table,
                                                           uint8_t* __restrict__ slots,
-                                                          uint32_t* __restrict__ cw) {
+                                                          uint32_t* __restrict__ cw, EncTail tail) {
   using Cfg = EncCfg<FT>;
   using WordT = typename Cfg::WordT;
   constexpr int S = Cfg::S, K = Cfg::K, V = Cfg::V;
@@ -427,9 +598,21 @@ __global__ __launch_bounds__(enc::kThreads) void k_encode(BatchDesc in, BatchDes
   __shared__ __attribute__((aligned(16))) uint8_t symS[Cfg::kHalfStreams][enc::kSegWords];
   __shared__ __attribute__((aligned(16))) uint16_t ringS[Cfg::kHalfStreams / 2][2 * enc::kRing];
   __shared__ uint32_t trashS[enc::kWaves][64];
+  constexpr bool kFused = S == 1;
+  __shared__ uint32_t cwE[Cfg::kBlocksPerWG];
+  __shared__ uint32_t preE[Cfg::kBlocksPerWG];
 
   const uint32_t b = batchOffset + blockIdx.y;
   const uint32_t tid = threadIdx.x;
+  const uint32_t n = in.size(b);
+  const uint32_t nBlocks = divUp(n, kBlockSize);
+  const uint32_t first = blockIdx.x * Cfg::kBlocksPerWG;
+  // workgroup 0 of an element always runs (headers, empty elements)
+  if (first >= nBlocks && (!kFused || blockIdx.x != 0)) return;
+  gp<uint8_t> base = startOf(out, b);
+  gp<uint8_t> o = base + (FT == 0 ? 0u : 32u + floatRawBytes(FT, n));  // ANS archive
+  gp<uint8_t> states = o + kANSHeaderBytes + kPdfBytes;
+  gp<uint2> bwords = (gp<uint2>)(states + uint64_t(kStateBytesPerBlock) * nBlocks);
 #pragma unroll
   for (int s = 0; s < S; ++s) {
     const uint4 t = ld16(G(table) + (uint64_t(s) * numInBatch + b) * kNumSymbols + tid);
@@ -437,11 +620,9 @@ __global__ __launch_bounds__(enc::kThreads) void k_encode(BatchDesc in, BatchDes
   }
   __syncthreads();
 
-  const uint32_t n = in.size(b);
-  const uint32_t nBlocks = divUp(n, kBlockSize);
   const uint32_t w = readfirst(tid >> 6), lane = tid & 63, h = lane >> 5, l = lane & 31;
-  const uint32_t blk0 = blockIdx.x * Cfg::kBlocksPerWG + w * Cfg::kBlocksPerWave;
-  if (blk0 >= nBlocks) return;
+  const uint32_t blk0 = first + w * Cfg::kBlocksPerWave;
+  if (blk0 < nBlocks) {
   uint32_t hv = h ? ~0u : 0u;
   asm volatile("" : "+v"(hv));  // keep `hv & x` a v_and
 
@@ -613,11 +794,43 @@ __global__ __launch_bounds__(enc::kThreads) void k_encode(BatchDesc in, BatchDes
       EStream& p = st[c][s];
       ringFlushAll(p, lane);
       if (uw[c]) {
-        gp<uint8_t> slot = G(slots) + ((uint64_t(s) * numInBatch + b) * MB + blk[c]) * kSlotBytes;
-        ((gp<uint32_t>)slot)[l] = p.x;
-        if (l == 0) G(cw)[(uint64_t(s) * numInBatch + b) * MB + blk[c]] = uint32_t(h ? p.nout[1] : p.nout[0]);
+        const uint32_t words = uint32_t(h ? p.nout[1] : p.nout[0]);
+        if constexpr (kFused) {
+          ((gp<uint32_t>)(states + uint64_t(kStateBytesPerBlock) * blk[c]))[l] = p.x;
+          if (l == 0) cwE[blk[c] - first] = words;
+        } else {
+          gp<uint8_t> slot = G(slots) + ((uint64_t(s) * numInBatch + b) * MB + blk[c]) * kSlotBytes;
+          ((gp<uint32_t>)slot)[l] = p.x;
+          if (l == 0) G(cw)[(uint64_t(s) * numInBatch + b) * MB + blk[c]] = words;
+        }
       }
     }
+  }
+  }  // blk0 < nBlocks
+  if constexpr (kFused) {
+    // every wave's slot stores are complete before other waves copy them
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const uint32_t nk = first < nBlocks ? min(uint32_t(Cfg::kBlocksPerWG), nBlocks - first) : 0u;
+    if (w == 0) {
+      const uint32_t r = lane < nk ? roundUp(cwE[lane], 8) : 0u;
+      const uint32_t inc = waveInclusiveScan(r);
+      const uint32_t agg = readfirst(__shfl(inc, 63));
+      const uint32_t excl = DG_EXP == 21 ? 0u : lookBack(G(tail.flags) + uint64_t(b) * tail.nW, blockIdx.x, agg);
+      if (lane < nk) preE[lane] = excl + inc - r;
+      if (lane == 0 && (first + Cfg::kBlocksPerWG >= nBlocks))
+        writeHeadTotal<FT>(base, o, n, nBlocks, excl + agg, bwords, tail, b);
+    }
+    if (blockIdx.x == 0) writeHeadFixed<FT>(base, o, n, nBlocks, tail, b);
+    __syncthreads();
+    if (tid < nk) {
+      const uint32_t k = first + tid;
+      const uint32_t uwk = min(kBlockSize, n - k * kBlockSize);
+      st8(bwords + k, make_uint2((uwk << 16) | cwE[tid], preE[tid]));
+    }
+    if (DG_EXP != 20)
+    copyPayload(preE, cwE, nk, G(slots) + (uint64_t(b) * MB + first) * kSlotBytes + kStateBytesPerBlock,
+                (gp<uint8_t>)(bwords + roundUp(nBlocks, 2)));
   }
 }
 
@@ -743,52 +956,9 @@ __global__ __launch_bounds__(kThreads) void k_coalesce(
     }
   }
   __syncthreads();
-  // payload: the workgroup's blocks are contiguous in the archive, so every
-  // thread copies 16 B vectors (8 words) across the whole range, the source
-  // block found by binary search over the LDS prefix; 4 vectors in flight
-  // per thread.  Words past a block's count are written as 0.
   const uint32_t nk = last > first ? last - first : 0;
-  if (nk == 0) return;
-  const uint32_t w0 = pre[0];
-  const uint32_t nv = (pre[nk - 1] + roundUp(cwL[nk - 1], 8) - w0) / 8;
-  gp<uint4> dst = (gp<uint4>)(data + 2ull * w0);
-  gp<const uint8_t> slot0 = G(slots) + ((uint64_t(seg) * numInBatch + b) * MB + first) * kSlotBytes +
-                            kStateBytesPerBlock;
-  constexpr int kIn = 4;
-  for (uint32_t v0 = tid; v0 < nv; v0 += kIn * kThreads) {
-    uint4 val[kIn];
-    uint32_t valid[kIn];
-#pragma unroll
-    for (int q = 0; q < kIn; ++q) {
-      const uint32_t v = v0 + q * kThreads;
-      valid[q] = 0;
-      if (v < nv) {
-        const uint32_t w = w0 + 8 * v;
-        uint32_t lo = 0, hi = nk;  // last k with pre[k] <= w
-        while (hi - lo > 1) {
-          const uint32_t mid = (lo + hi) >> 1;
-          if (pre[mid] <= w) lo = mid; else hi = mid;
-        }
-        const uint32_t off = w - pre[lo];
-        valid[q] = cwL[lo] > off ? cwL[lo] - off : 0;
-        val[q] = ld16((gp<const uint4>)(slot0 + uint64_t(lo) * kSlotBytes + 2ull * off));
-      }
-    }
-#pragma unroll
-    for (int q = 0; q < kIn; ++q) {
-      const uint32_t v = v0 + q * kThreads;
-      if (v >= nv) continue;
-      uint4 x = val[q];
-      if (valid[q] < 8) {
-        uint32_t* vw = reinterpret_cast<uint32_t*>(&x);
-#pragma unroll
-        for (uint32_t r = 0; r < 4; ++r) {
-          if (2 * r + 1 >= valid[q]) vw[r] &= (2 * r < valid[q]) ? 0xffffu : 0u;
-        }
-      }
-      st16(dst + v, x);
-    }
-  }
+  copyPayload(pre, cwL, nk, G(slots) + ((uint64_t(seg) * numInBatch + b) * MB + first) * kSlotBytes +
+                                kStateBytesPerBlock, data);
 }
 
 // ---------------------------------------------------------------------------

@@ -134,7 +134,9 @@ struct StagingRing {
       return e;
     }
     hipEvent_t e;
-    HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    // completion of the copy is all the ring needs: no system-scope fence
+    // (it would write back and invalidate L2 at every upload)
+    HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventDisableSystemFence));
     return e;
   }
   // Uses are allocated in address order around the ring, so the oldest use is
