@@ -13,6 +13,9 @@
 #include <sstream>
 #include <vector>
 
+#ifndef DG_EXP
+#define DG_EXP 0  // timing experiments only (make exp)
+#endif
 #include "codec_internal.h"
 #include "dietgpu/GpuANSCodec.h"
 #include "dietgpu/GpuFloatCodec.h"
@@ -27,7 +30,8 @@ constexpr uint32_t kMaxGridY = 65535;
 
 uint32_t histChunkWords(uint32_t nb, uint32_t maxSize) {
   uint32_t chunk = 64 * 1024;
-  while (chunk > 4096 && uint64_t(nb) * divUp(std::max(maxSize, 1u), chunk) < 2048) chunk /= 2;
+  const uint32_t target = DG_EXP == 30 ? 4096 : DG_EXP == 31 ? 8192 : DG_EXP == 32 ? 16384 : 2048;
+  while (chunk > 4096 && uint64_t(nb) * divUp(std::max(maxSize, 1u), chunk) < target) chunk /= 2;
   while (divUp(maxSize, chunk) > 4096) chunk *= 2;
   return chunk;
 }

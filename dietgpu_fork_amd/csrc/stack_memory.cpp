@@ -161,8 +161,11 @@ StagingRing& ring() {
 }
 } // namespace
 
+bool uploadViaKernargs(void* dst, const void* src, size_t bytes, hipStream_t s);  // upload.hip
+
 void StackDeviceMemory::copyToDevice(void* dst, const void* src, size_t bytes, hipStream_t s) {
   if (!bytes) return;
+  if (uploadViaKernargs(dst, src, bytes, s)) return;  // tables up to 64 KB: no blit
   auto& r = ring();
   if (bytes > StagingRing::kBytes / 4) {
     HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s));
