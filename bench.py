@@ -41,6 +41,8 @@ def parse():
                    help="tensors of the batch timed on the CPU oracle (rank 0, N=1)")
     p.add_argument("--no-kernel-events", action="store_true",
                    help="time without per-kernel hipEvents (diagnostic)")
+    p.add_argument("--no-extras", dest="extras", action="store_false",
+                   help="skip the secondary configs (c3 bytes, c4 fp64 / sparse, fp32 batch)")
     p.add_argument("--no-verify", dest="verify", action="store_false",
                    help="skip the round-trip check (kernel-variant timing experiments only)")
     return p.parse_args()
@@ -197,10 +199,134 @@ def main():
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = _cpu_baseline(x, min(args.cpu_sample, nb), pb)
+    if world == 1 and args.extras:
+        del comp, out, x, ws
+        torch.cuda.empty_cache()
+        line["extras"] = _extras(dev, pb)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def _timed(fn, reps):
+    """Average ms of fn() over reps calls (torch events on the current stream,
+    which is the stream the C ABI launches on)."""
+    import torch
+
+    fn()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(reps):
+        fn()
+    b.record()
+    b.synchronize()
+    return a.elapsed_time(b) / reps
+
+
+def _extras(dev, pb, reps=3):
+    """Secondary BASELINE configs on this GPU (not the headline): whole-call
+    compress and decompress times (every kernel of the call, inputs resident
+    in HBM), ratio, and a bit-exact roundtrip check.  U/t is the reference's
+    GB/s convention; `algorithmic_GBps` is 2(U + C) / (t_c + t_d)."""
+    import torch
+
+    from dietgpu_fork_amd import codec as C
+
+    out = []
+
+    fams = ("hist", "normalize", "encode", "coalesce", "decode", "sparse")
+
+    def breakdown(fc, fd):
+        """avg ms per launch of each kernel family in one extra profiled call
+        of each direction (event pairs around every launch)"""
+        r = {}
+        for tag, fn in (("c", fc), ("d", fd)):
+            torch.cuda.synchronize()
+            C.profile_reset()
+            C.profile_filter(None)
+            C.profile(True)
+            fn()
+            torch.cuda.synchronize()
+            C.profile(False)
+            for k in fams:
+                ms, launches = C.profile_query(k)
+                if launches:
+                    r[f"{tag}:{k}"] = round(ms / launches, 4)
+        return r
+
+    def record(name, U, C_bytes, tc, td, exact, **kw):
+        out.append({"config": name, "uncompressed_bytes": U, "ratio": round(C_bytes / U, 5),
+                    "compress_ms": round(tc, 3), "decompress_ms": round(td, 3),
+                    "compress_GBps": round(U / tc / 1e6, 1), "decompress_GBps": round(U / td / 1e6, 1),
+                    "encode_plus_decode_GBps": round(U / (tc + td) / 1e6, 1),
+                    "algorithmic_GBps": round(2 * (U + C_bytes) / (tc + td) / 1e6, 1),
+                    "roundtrip_bit_exact": bool(exact), **kw})
+
+    # c3: 1024 x 4 MiB bytes, uniform over 16 symbols (4.0 bit/sym)
+    nb, n = 1024, 4 << 20
+    g = torch.Generator(device=dev).manual_seed(3)
+    x = torch.randint(0, 16, (nb, n), generator=g, device=dev, dtype=torch.uint8)
+    ws = C.Workspace(7 << 30, dev)
+    arch, sizes = C.ans_encode_stride(x, prob_bits=pb, ws=ws)
+    y, ok, _ = C.ans_decode_stride(arch, n, prob_bits=pb, ws=ws)
+    tc = _timed(lambda: C.ans_encode_stride(x, prob_bits=pb, ws=ws, out=arch, sizes=sizes), reps)
+    td = _timed(lambda: C.ans_decode_stride(arch, n, prob_bits=pb, ws=ws, out=y), reps)
+    exact = bool((ok == 1).all()) and torch.equal(x, y)
+    kern = breakdown(lambda: C.ans_encode_stride(x, prob_bits=pb, ws=ws, out=arch, sizes=sizes),
+                     lambda: C.ans_decode_stride(arch, n, prob_bits=pb, ws=ws, out=y))
+    record("c3: 1024 x 4 MiB bytes, 4 bit/sym (ansEncodeBatchStride / ansDecodeBatchStride)",
+           nb * n, int(sizes.to(torch.int64).sum()), tc, td, exact, kernels_ms=kern)
+    del x, y, arch, ws
+    torch.cuda.empty_cache()
+
+    # float batches of the c2 shape in the other float types
+    for dt, words in ((torch.float32, 262144), (torch.float16, 524288)):
+        g = torch.Generator(device=dev).manual_seed(11)
+        x = torch.randn(256, words, generator=g, device=dev).to(dt)
+        ws = C.Workspace(1 << 30, dev)
+        arch, sizes = C.float_compress_stride(x, prob_bits=pb, ws=ws)
+        y, ok, _ = C.float_decompress_stride(arch, words, dt, prob_bits=pb, ws=ws)
+        tc = _timed(lambda: C.float_compress_stride(x, prob_bits=pb, ws=ws, out=arch, sizes=sizes), reps)
+        td = _timed(lambda: C.float_decompress_stride(arch, words, dt, prob_bits=pb, ws=ws, out=y), reps)
+        exact = bool((ok == 1).all()) and torch.equal(x.view(torch.uint8), y.view(torch.uint8))
+        kern = breakdown(lambda: C.float_compress_stride(x, prob_bits=pb, ws=ws, out=arch, sizes=sizes),
+                         lambda: C.float_decompress_stride(arch, words, dt, prob_bits=pb, ws=ws, out=y))
+        record(f"256 x 1 MiB {str(dt)[6:]} N(0,1) (floatCompress stride)", x.numel() * x.element_size(),
+               int(sizes.to(torch.int64).sum()), tc, td, exact, kernels_ms=kern)
+        del x, y, arch, ws
+
+    # c4: fp64 two-pass (16,777,216 words) and 90 %-sparse fp32 (15,000,000)
+    g = torch.Generator(device=dev).manual_seed(4)
+    x = torch.randn(16777216, generator=g, device=dev, dtype=torch.float64)
+    ws = C.Workspace(2 << 30, dev)
+    arch, sizes = C.float_compress_pointer([x], prob_bits=pb, ws=ws)
+    y = torch.empty_like(x)
+    row = [arch[0]]
+    ok, _ = C.float_decompress_pointer(row, [y], prob_bits=pb, ws=ws)
+    tc = _timed(lambda: C.float_compress_pointer([x], prob_bits=pb, ws=ws), reps)
+    td = _timed(lambda: C.float_decompress_pointer(row, [y], prob_bits=pb, ws=ws), reps)
+    exact = int(ok[0]) == 1 and torch.equal(x.view(torch.int64), y.view(torch.int64))
+    kern = breakdown(lambda: C.float_compress_pointer([x], prob_bits=pb, ws=ws),
+                     lambda: C.float_decompress_pointer(row, [y], prob_bits=pb, ws=ws))
+    record("c4: 1 x 128 MiB fp64 N(0,1), two ANS passes", x.numel() * 8, int(sizes[0]), tc, td, exact,
+           kernels_ms=kern)
+    g = torch.Generator(device=dev).manual_seed(5)
+    f = torch.randn(15000000, generator=g, device=dev)
+    f[torch.rand(f.numel(), generator=g, device=dev) < 0.9] = 0.0
+    arch, sizes = C.sparse_compress([f], prob_bits=pb, ws=ws)
+    y = torch.empty_like(f)
+    row = [arch[0]]
+    ok, _ = C.sparse_decompress(row, [y], prob_bits=pb, ws=ws)
+    tc = _timed(lambda: C.sparse_compress([f], prob_bits=pb, ws=ws), reps)
+    td = _timed(lambda: C.sparse_decompress(row, [y], prob_bits=pb, ws=ws), reps)
+    exact = int(ok[0]) == 1 and torch.equal(f.view(torch.int32), y.view(torch.int32))
+    kern = breakdown(lambda: C.sparse_compress([f], prob_bits=pb, ws=ws),
+                     lambda: C.sparse_decompress(row, [y], prob_bits=pb, ws=ws))
+    record("c4: 1 x 15M fp32, 90 % zeros (sparse bitmap + dense codec)", f.numel() * 4, int(sizes[0]),
+           tc, td, exact, kernels_ms=kern)
+    return out
 
 
 def _pmc_traffic(kernel, U, comp):

@@ -71,6 +71,11 @@ void encodeBatchDevice(StackDeviceMemory& res, int pb, bool useChecksum, uint32_
 
   auto partHist = res.alloc<uint32_t>(s, runHist ? size_t(kSegs) * nb * chunks * kNumSymbols : 1);
   auto partCk = res.alloc<uint32_t>(s, rawCk ? size_t(nb) * chunks : 1);
+  // first-level sums when elements have many chunks (k_histReduce)
+  const uint32_t groups = divUp(chunks, kReduceRows);
+  const bool reduce2 = runHist && chunks > kReduceRows;
+  auto groupHist = res.alloc<uint32_t>(s, reduce2 ? size_t(kSegs) * nb * groups * kNumSymbols : 1);
+  auto groupCk = res.alloc<uint32_t>(s, reduce2 && rawCk ? size_t(nb) * groups : 1);
   auto ck = res.alloc<uint32_t>(s, nb);
   auto table = res.alloc<uint4>(s, size_t(kSegs) * nb * kNumSymbols);
   auto pdf = res.alloc<uint16_t>(s, size_t(kSegs) * nb * kNumSymbols);
@@ -104,12 +109,29 @@ void encodeBatchDevice(StackDeviceMemory& res, int pb, bool useChecksum, uint32_
       k_checksum<<<g, kThreads, 0, s>>>(in, y0, 1, ckChunk, ck.data());
       HIP_LAUNCH_CHECK();
     }
+    const uint32_t* histRows = userHist ? hist_dev : partHist.data();
+    const uint32_t* ckRows = rawCk ? partCk.data() : nullptr;
+    uint32_t nHistRows = userHist ? 1u : chunks, nCkRows = chunks;
+    if (reduce2) {
+      prof::Scope p("normalize", s);
+      dim3 g(groups, ny, kSegs);
+      k_histReduce<<<g, kThreads, 0, s>>>(y0, nb, chunks, groups, partHist.data(), ckRows,
+                                          groupHist.data(), rawCk ? groupCk.data() : nullptr);
+      HIP_LAUNCH_CHECK();
+      if (!userHist) {
+        histRows = groupHist.data();
+        nHistRows = groups;
+      }
+      if (rawCk) {
+        ckRows = groupCk.data();
+        nCkRows = groups;
+      }
+    }
     {
       prof::Scope p("normalize", s);
       dim3 g(ny, kSegs);
-      k_normalize<<<g, kThreads, 0, s>>>(in, y0, nb, userHist ? hist_dev : partHist.data(),
-                                         userHist ? 1u : chunks, pb, table.data(), pdf.data(),
-                                         rawCk ? partCk.data() : nullptr, ck.data(),
+      k_normalize<<<g, kThreads, 0, s>>>(in, y0, nb, histRows, nHistRows, pb, table.data(),
+                                         pdf.data(), ckRows, nCkRows, ck.data(),
                                          kFused ? flags.data() : nullptr, nW);
       HIP_LAUNCH_CHECK();
     }

@@ -152,6 +152,44 @@ __global__ __launch_bounds__(kThreads) void k_hist(BatchDesc in, uint32_t batchO
 }
 
 // ---------------------------------------------------------------------------
+// k_histReduce: first level of the partial-histogram sum when an element has
+// many chunks (few large elements: one 128 MiB fp64 tensor is 2048 chunks,
+// which k_normalize's single workgroup would sum serially for ~0.3 ms).
+// grid (groups, batch, segments): workgroup g sums chunks [64g, 64g + 64) of
+// its (element, segment) row, and the byte-checksum partials likewise.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kReduceRows = 64;
+
+static __global__ __launch_bounds__(kThreads) void k_histReduce(
+    uint32_t batchOffset, uint32_t numInBatch, uint32_t chunksPerElem, uint32_t groups,
+    const uint32_t* __restrict__ part, const uint32_t* __restrict__ partCk,
+    uint32_t* __restrict__ outHist, uint32_t* __restrict__ outCk) {
+  const uint32_t b = batchOffset + blockIdx.y;
+  const uint32_t g = blockIdx.x;
+  const uint64_t row = uint64_t(blockIdx.z) * numInBatch + b;
+  const uint32_t c0 = g * kReduceRows;
+  const uint32_t c1 = min(chunksPerElem, c0 + kReduceRows);
+  gp<const uint32_t> hp = G(part) + (row * chunksPerElem) * kNumSymbols + threadIdx.x;
+  uint32_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint32_t c = c0;
+  for (; c + 8 <= c1; c += 8) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc[k] += hp[uint64_t(c + k) * kNumSymbols];
+  }
+  for (; c < c1; ++c) acc[0] += hp[uint64_t(c) * kNumSymbols];
+  uint32_t sum = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) sum += acc[k];
+  G(outHist)[(row * groups + g) * kNumSymbols + threadIdx.x] = sum;
+  if (partCk && blockIdx.z == 0 && threadIdx.x < 64) {
+    uint32_t ck = 0;
+    for (uint32_t k = c0 + threadIdx.x; k < c1; k += 64) ck ^= G(partCk)[uint64_t(b) * chunksPerElem + k];
+    ck = waveXor(ck);
+    if (threadIdx.x == 0) G(outCk)[uint64_t(b) * groups + g] = ck;
+  }
+}
+
+// ---------------------------------------------------------------------------
 // k_normalize: one workgroup per (element, segment).  Bit-exact restatement of
 // normalizeProbabilitiesFromHistogram (ans/GpuANSStatistics.cuh:178-366):
 // float32 quantisation, descending order of the unique keys (q << 16) | sym
@@ -166,8 +204,8 @@ __global__ __launch_bounds__(kThreads) void k_hist(BatchDesc in, uint32_t batchO
 static __global__ __launch_bounds__(kThreads) void k_normalize(
     BatchDesc in, uint32_t batchOffset, uint32_t numInBatch, const uint32_t* __restrict__ hist,
     uint32_t chunksPerElem, int pb, uint4* __restrict__ table, uint16_t* __restrict__ pdfOut,
-    const uint32_t* __restrict__ partCk, uint32_t* __restrict__ ckOut, uint64_t* __restrict__ flags,
-    uint32_t nW) {
+    const uint32_t* __restrict__ partCk, uint32_t ckChunks, uint32_t* __restrict__ ckOut,
+    uint64_t* __restrict__ flags, uint32_t nW) {
   __shared__ uint32_t keys[kNumSymbols];
   __shared__ uint32_t red[kWaves];
   const uint32_t b = batchOffset + blockIdx.x;
@@ -179,11 +217,12 @@ static __global__ __launch_bounds__(kThreads) void k_normalize(
 
   if (partCk && seg == 0 && s == 0) {
     uint32_t ck = 0;
-    for (uint32_t c = 0; c < chunksPerElem; ++c) ck ^= G(partCk)[uint64_t(b) * chunksPerElem + c];
+    for (uint32_t c = 0; c < ckChunks; ++c) ck ^= G(partCk)[uint64_t(b) * ckChunks + c];
     G(ckOut)[b] = ck;
   }
   uint32_t count = 0;
   gp<const uint32_t> hp = G(hist) + row * chunksPerElem * kNumSymbols + s;
+#pragma unroll 8
   for (uint32_t c = 0; c < chunksPerElem; ++c) count += hp[uint64_t(c) * kNumSymbols];
 
   const uint32_t total = in.size(b);

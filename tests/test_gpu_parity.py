@@ -89,6 +89,20 @@ def test_ans_user_histogram(C, ws):
     np.testing.assert_array_equal(out[0, : int(sizes[0])].cpu().numpy(), ref)
 
 
+@pytest.mark.parametrize("user_hist", [False, True])
+def test_ans_large_single_checksum(C, ws, user_hist):
+    """One 6 MB element: ~1500 histogram chunks, so the partial histograms and
+    byte-checksum partials go through the two-level reduction (k_histReduce)."""
+    d = exp_bytes(6_000_000, lam=10.0, seed=9)
+    t = torch.from_numpy(d).to(DEV).view(1, -1)
+    h = torch.from_numpy(O.histogram(d).astype(np.int32)).to(DEV) if user_hist else None
+    out, sizes = C.ans_encode_stride(t, ws=ws, histogram=h, checksum=True)
+    ref = O.ans_encode(d, 10, True)
+    np.testing.assert_array_equal(out[0, : int(sizes[0])].cpu().numpy(), ref)
+    dec, ok, _ = C.ans_decode_stride(out, d.size, ws=ws, checksum=True)
+    assert int(ok[0]) == 1 and np.array_equal(dec[0].cpu().numpy(), d)
+
+
 def test_ans_uniform_16_symbols(C, ws):
     # c3 shape (4.0 bit / symbol), reduced batch
     rng = np.random.default_rng(3)
