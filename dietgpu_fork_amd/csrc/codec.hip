@@ -45,6 +45,9 @@ uint32_t residentSlots(const void* kernel, int threads, uint32_t dynLds) {
   return uint32_t(std::max(1, cus) * std::max(1, perCU));
 }
 
+// below this many block-pair chains a decode runs one chain per wave
+constexpr uint64_t kSmallBatchChains = 8192;
+
 void checkProbBits(int pb) {
   DG_CHECK(pb >= 9 && pb <= 11, "unhandled pdf precision " << pb << " (must be 9, 10 or 11)");
 }
@@ -162,18 +165,31 @@ void decodeBatchDevice(StackDeviceMemory& res, int pb, uint32_t nb, const BatchD
   checkProbBits(pb);
   if (nb == 0) return;
   const uint32_t maxBlocks = divUp(maxCapacity, kBlockSize);
-  for (uint32_t y0 = 0; y0 < nb; y0 += kMaxGridY) {
-    const uint32_t ny = std::min(kMaxGridY, nb - y0);
-    prof::Scope p("decode", s);
-    // one generation of resident workgroups; each decodes P chunks
-    const uint32_t lds = DecCfg<FT>::ldsBytes(pb);
-    const uint32_t chunks = std::max(1u, divUp(maxBlocks, DecCfg<FT>::kBlocksPerWG));
-    const uint32_t slots = residentSlots(reinterpret_cast<const void*>(&k_decode<FT>), dec::kThreads, lds);
-    const uint32_t P = std::max(1u, uint32_t((uint64_t(chunks) * ny + slots / 2) / slots));
-    dim3 g(divUp(chunks, P), ny);
-    k_decode<FT><<<g, dec::kThreads, lds, s>>>(in, out, y0, pb, P, outSuccess_dev, outSize_dev);
-    HIP_LAUNCH_CHECK();
-  }
+  auto launch = [&](auto kTag) {
+    constexpr int KK = decltype(kTag)::value;
+    using Cfg = DecCfg<FT, KK>;
+    for (uint32_t y0 = 0; y0 < nb; y0 += kMaxGridY) {
+      const uint32_t ny = std::min(kMaxGridY, nb - y0);
+      prof::Scope p("decode", s);
+      // one generation of resident workgroups; each decodes P chunks
+      const uint32_t lds = Cfg::ldsBytes(pb);
+      const uint32_t chunks = std::max(1u, divUp(maxBlocks, Cfg::kBlocksPerWG));
+      const uint32_t slots =
+          residentSlots(reinterpret_cast<const void*>(&k_decode<FT, KK>), dec::kThreads, lds);
+      const uint32_t P = std::max(1u, uint32_t((uint64_t(chunks) * ny + slots / 2) / slots));
+      dim3 g(divUp(chunks, P), ny);
+      k_decode<FT, KK><<<g, dec::kThreads, lds, s>>>(in, out, y0, pb, P, outSuccess_dev, outSize_dev);
+      HIP_LAUNCH_CHECK();
+    }
+  };
+  // Independent chains in the batch (one per block pair and ANS stream).
+  // The throughput shape runs 4 per wave; with fewer than 2 per SIMD-slot of
+  // one generation at that shape (~8192 on 256 CUs) one per wave is faster.
+  const uint64_t chains = uint64_t(nb) * divUp(maxBlocks, 2) * FloatTraits<FT>::kSegs;
+  if (chains < kSmallBatchChains)
+    launch(std::integral_constant<int, 1>{});
+  else
+    launch(std::integral_constant<int, 0>{});
 }
 
 // Verify stored checksums against `unitBytes * out.size(b)` decoded bytes

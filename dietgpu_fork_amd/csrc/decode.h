@@ -69,10 +69,13 @@ constexpr uint32_t kUnroll = 4;      // steps between ring checks
 constexpr uint32_t kChunk = kSegWords / 32;  // words joined per lane per segment
 }  // namespace dec
 
-template <int FT>
+// KK = 0: the throughput shape (4 chains per wave); KK = 1: one block pair
+// per wave, for batches with too few block pairs to fill the chip that way
+// (a single large tensor): the same chains spread over 4x the SIMDs.
+template <int FT, int KK = 0>
 struct DecCfg {
   static constexpr int S = FloatTraits<FT>::kSegs;  // ANS streams per word
-  static constexpr int K = S == 2 ? 2 : 4;          // block pairs per wave
+  static constexpr int K = KK ? KK : (S == 2 ? 2 : 4);  // block pairs per wave
   static constexpr int kBlocksPerWave = 2 * K;
   static constexpr int kBlocksPerWG = dec::kWaves * kBlocksPerWave;
   static constexpr uint32_t kHalfStreams = dec::kWaves * K * S * 2;
@@ -324,13 +327,13 @@ __device__ __forceinline__ void buildLut64(gp<const uint16_t> pdfIn, lp<u32x2> l
 // grid (ceil(maxBlocks / (kBlocksPerWG * chunksPerWG)), batch), dynamic LDS
 // DecCfg<FT>::ldsBytes(pb).  out.size(b) = capacity (bytes for raw ANS,
 // words for floats).
-template <int FT>
+template <int FT, int KK>
 __global__ __launch_bounds__(dec::kThreads) void k_decode(BatchDesc in, BatchDesc out,
                                                           uint32_t batchOffset, int pb,
                                                           uint32_t chunksPerWG,
                                                           uint8_t* __restrict__ outSuccess,
                                                           uint32_t* __restrict__ outSize) {
-  using Cfg = DecCfg<FT>;
+  using Cfg = DecCfg<FT, KK>;
   using WordT = typename FloatTraits<FT>::WordT;
   constexpr int S = Cfg::S, K = Cfg::K, R = Join<FT>::kR;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];

@@ -160,6 +160,22 @@ def test_c4_fp64_and_sparse(C, ws):
     assert int(ok[0]) == 1 and torch.equal(f.view(torch.int32), y.view(torch.int32))
 
 
+@pytest.mark.parametrize("ft,nb,n", [(1, 256, 262144), (3, 256, 262144), (4, 64, 524288)])
+def test_throughput_shape_other_floats(C, ws, ft, nb, n):
+    """Batches with >= 8192 block-pair chains take the 4-chains-per-wave decode
+    (smaller ones one chain per wave, covered by the parity tests)."""
+    g = torch.Generator(device=DEV).manual_seed(20 + ft)
+    x = torch.randn(nb, n, generator=g, device=DEV, dtype=torch.float64).to(FLOAT_DT[ft])
+    out, sizes = C.float_compress_stride(x, prob_bits=10, ws=ws)
+    s = sizes.cpu().numpy().astype(np.int64)
+    y, ok, sz = C.float_decompress_stride(out, n, FLOAT_DT[ft], ws=ws)
+    assert bool((ok == 1).all()) and bool((sz == n).all())
+    assert torch.equal(y.view(torch.uint8), x.view(torch.uint8))
+    i = nb // 3
+    ref = O.float_compress(x[i].cpu().numpy().view(NP_WORD[ft]), ft, 10)
+    np.testing.assert_array_equal(out[i, : s[i]].cpu().numpy(), ref)
+
+
 # --- torch.ops.dietgpu (DietGpu.cpp) ------------------------------------------
 
 def test_torch_ops_float_roundtrip(C):
