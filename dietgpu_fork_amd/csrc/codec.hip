@@ -45,9 +45,6 @@ uint32_t residentSlots(const void* kernel, int threads, uint32_t dynLds) {
   return uint32_t(std::max(1, cus) * std::max(1, perCU));
 }
 
-// below this many block-pair chains a decode runs one chain per wave
-constexpr uint64_t kSmallBatchChains = 8192;
-
 void checkProbBits(int pb) {
   DG_CHECK(pb >= 9 && pb <= 11, "unhandled pdf precision " << pb << " (must be 9, 10 or 11)");
 }
@@ -142,7 +139,7 @@ void encodeBatchDevice(StackDeviceMemory& res, int pb, bool useChecksum, uint32_
       prof::Scope p("encode", s);
       dim3 g(nW, ny);
       const EncTail tail{pdf.data(), ck.data(), outSize_dev, flags.data(), nW, pb, useChecksum};
-      k_encode<FT><<<g, enc::kThreads, 0, s>>>(in, out, y0, nb, std::max(MB, 1u), table.data(),
+      k_encode<FT, 0><<<g, enc::kThreads, 0, s>>>(in, out, y0, nb, std::max(MB, 1u), table.data(),
                                                slots.data(), cw.data(), tail);
       HIP_LAUNCH_CHECK();
     }
@@ -182,14 +179,7 @@ void decodeBatchDevice(StackDeviceMemory& res, int pb, uint32_t nb, const BatchD
       HIP_LAUNCH_CHECK();
     }
   };
-  // Independent chains in the batch (one per block pair and ANS stream).
-  // The throughput shape runs 4 per wave; with fewer than 2 per SIMD-slot of
-  // one generation at that shape (~8192 on 256 CUs) one per wave is faster.
-  const uint64_t chains = uint64_t(nb) * divUp(maxBlocks, 2) * FloatTraits<FT>::kSegs;
-  if (chains < kSmallBatchChains)
-    launch(std::integral_constant<int, 1>{});
-  else
-    launch(std::integral_constant<int, 0>{});
+  launch(std::integral_constant<int, 0>{});
 }
 
 // Verify stored checksums against `unitBytes * out.size(b)` decoded bytes
@@ -650,7 +640,7 @@ void floatGetCompressedInfo(StackDeviceMemory& res, const void** in, uint32_t nu
 
 }  // namespace dietgpu
 
-#if DG_EXP == 7
+#if DG_EXP == 7 || defined(DG_TRACE)
 extern "C" int dietgpu_debug_read(void* dst, size_t bytes) {
   return hipMemcpyFromSymbol(dst, HIP_SYMBOL(dietgpu::g_dbgT), bytes, 0, hipMemcpyDeviceToHost) == hipSuccess
              ? 0

@@ -34,7 +34,7 @@
 #endif
 
 namespace dietgpu {
-#if DG_EXP == 7
+#if DG_EXP == 7 || defined(DG_TRACE)
 // experiment 7: per-wave s_memtime stamps (lane 0), 24 slots per wave
 __device__ uint64_t g_dbgT[16384 * 24];
 #define DG_STAMP(slot)                                                                \
@@ -69,13 +69,14 @@ constexpr uint32_t kUnroll = 4;      // steps between ring checks
 constexpr uint32_t kChunk = kSegWords / 32;  // words joined per lane per segment
 }  // namespace dec
 
-// KK = 0: the throughput shape (4 chains per wave); KK = 1: one block pair
-// per wave, for batches with too few block pairs to fill the chip that way
-// (a single large tensor): the same chains spread over 4x the SIMDs.
+// KK: block pairs per wave (0 = the default, 1).  One pair per wave beats
+// 2-4 interleaved pairs per wave at every batch size measured (c2 decode
+// 125 -> 102 us, c3 3.0 -> 2.3 ms): more, smaller waves hide the step's
+// latency better and fill the chip without generation quantisation.
 template <int FT, int KK = 0>
 struct DecCfg {
   static constexpr int S = FloatTraits<FT>::kSegs;  // ANS streams per word
-  static constexpr int K = KK ? KK : (S == 2 ? 2 : 4);  // block pairs per wave
+  static constexpr int K = KK ? KK : 1;             // block pairs per wave
   static constexpr int kBlocksPerWave = 2 * K;
   static constexpr int kBlocksPerWG = dec::kWaves * kBlocksPerWave;
   static constexpr uint32_t kHalfStreams = dec::kWaves * K * S * 2;
@@ -201,6 +202,18 @@ __device__ __forceinline__ void decStepAll(DStream* const (&p)[NC], const bool (
 #pragma unroll
   for (int c = 0; c < NC; ++c)
     p[c]->x = __builtin_amdgcn_perm(xn[c], v[c], rd[c] ? 0x05040100u : 0x07060504u);
+}
+
+// Wave priority from the share of the wave's work still ahead (wave-uniform
+// q in [0, 3]): the SIMD arbiter otherwise favours the oldest waves, so waves
+// that started together finish up to ~35 % apart and the kernel ends on a
+// tail with too few waves left to hide latency.
+__device__ __forceinline__ void setPrioRemaining(uint32_t left, uint32_t total) {
+  const uint32_t q = total ? min(3u, (4u * left) / total) : 0u;
+  if (q == 3) __builtin_amdgcn_s_setprio(3);
+  else if (q == 2) __builtin_amdgcn_s_setprio(2);
+  else if (q == 1) __builtin_amdgcn_s_setprio(1);
+  else __builtin_amdgcn_s_setprio(0);
 }
 
 // Join 8 decoded symbols (u16 sym << 8 in LDS) with their raw bytes.
@@ -556,6 +569,8 @@ __global__ __launch_bounds__(dec::kThreads) void k_decode(BatchDesc in, BatchDes
       // full segments: unrolled, unmasked
       DG_STAMP(1);
       auto fullSeg = [&](int32_t g, const uint32_t (&cur)[K][R], uint32_t (&nxt)[K][R]) {
+        if (DG_EXP != 64)  // (64: without, for A/B runs)
+          setPrioRemaining((chunksPerWG - 1 - pass) * uint32_t(nSeg) + uint32_t(g), chunksPerWG * uint32_t(nSeg));
         if (g > 0) loadRaw(g - 1, true, nxt);
 #pragma unroll
         for (int grp = int(dec::kSegSteps / dec::kUnroll) - 1; grp >= 0; --grp) {

@@ -294,11 +294,13 @@ constexpr uint32_t kFlush = 256;   // words per flush (64 lanes x 8 B)
 constexpr uint32_t kUnroll = 4;    // steps between flush checks
 }  // namespace enc
 
-template <int FT>
+// KK: block pairs per wave (0 = the default, 1; see decode.h DecCfg: c2
+// encode 111 -> 97 us against 2 pairs per wave).
+template <int FT, int KK = 0>
 struct EncCfg {
   using WordT = typename FloatTraits<FT>::WordT;
   static constexpr int S = FloatTraits<FT>::kSegs;
-  static constexpr int K = S == 2 ? 1 : 2;
+  static constexpr int K = KK ? KK : 1;
   static constexpr int kBlocksPerWave = 2 * K;
   static constexpr int kBlocksPerWG = enc::kWaves * kBlocksPerWave;
   // 16-byte input vectors per lane per block per segment (32 lanes x V x 16 B
@@ -623,14 +625,14 @@ __device__ void writeHeadTotal(gp<uint8_t> base, gp<uint8_t> o, uint32_t n, uint
 // (kFused): writes the whole archive (states straight to it, words via the
 // slots, see EncTail).  fp64: writes per block slot states, slot words and
 // cw[] (word count) for k_coalesce.
-template <int FT>
+template <int FT, int KK>
 __global__ __launch_bounds__(enc::kThreads) void k_encode(BatchDesc in, BatchDesc out,
                                                           uint32_t batchOffset,
                                                           uint32_t numInBatch, uint32_t MB,
                                                           const uint4* __restrict__ table,
                                                           uint8_t* __restrict__ slots,
                                                           uint32_t* __restrict__ cw, EncTail tail) {
-  using Cfg = EncCfg<FT>;
+  using Cfg = EncCfg<FT, KK>;
   using WordT = typename Cfg::WordT;
   constexpr int S = Cfg::S, K = Cfg::K, V = Cfg::V;
   __shared__ __attribute__((aligned(16))) uint32_t tblS[S][kNumSymbols * 4];

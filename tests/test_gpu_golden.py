@@ -162,8 +162,9 @@ def test_c4_fp64_and_sparse(C, ws):
 
 @pytest.mark.parametrize("ft,nb,n", [(1, 256, 262144), (3, 256, 262144), (4, 64, 524288)])
 def test_throughput_shape_other_floats(C, ws, ft, nb, n):
-    """Batches with >= 8192 block-pair chains take the 4-chains-per-wave decode
-    (smaller ones one chain per wave, covered by the parity tests)."""
+    """Large fp16 / fp32 / fp64 batches (multi-generation grids, persistent
+    decode workgroups with several chunks each): bit-exact round trip and
+    byte identity with the oracle on a sampled element."""
     g = torch.Generator(device=DEV).manual_seed(20 + ft)
     x = torch.randn(nb, n, generator=g, device=DEV, dtype=torch.float64).to(FLOAT_DT[ft])
     out, sizes = C.float_compress_stride(x, prob_bits=10, ws=ws)

@@ -9,7 +9,9 @@ import numpy as np
 import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-os.environ["DIETGPU_AMD_LIB"] = os.path.join(ROOT, "dietgpu_fork_amd/_lib/exp/libdietgpu_amd_exp7.so")
+# argv[1]: library built with the stamps (make exp EXP=7, or EXP=k EXPFLAGS=-DDG_TRACE)
+LIB = sys.argv[1] if len(sys.argv) > 1 else "libdietgpu_amd_exp7.so"
+os.environ["DIETGPU_AMD_LIB"] = os.path.join(ROOT, "dietgpu_fork_amd/_lib/exp", LIB)
 sys.path.insert(0, ROOT)
 from dietgpu_fork_amd import _native as N  # noqa: E402
 from dietgpu_fork_amd import codec as C  # noqa: E402
@@ -36,7 +38,8 @@ for _ in range(3):
     N.check(L.dietgpu_float_decompress(ws.h, 2, pb, 0, nb, comp_ptrs, out_ptrs, u, ok.data_ptr(),
                                        osz.data_ptr(), stream))
 torch.cuda.synchronize()
-assert torch.equal(out.view(torch.int16), x.view(torch.int16))
+if LIB.endswith("exp7.so"):  # timing-only variants decode garbage
+    assert torch.equal(out.view(torch.int16), x.view(torch.int16))
 buf = np.zeros(16384 * 24, dtype=np.uint64)
 L.dietgpu_debug_read.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
 assert L.dietgpu_debug_read(buf.ctypes.data, buf.nbytes) == 0
