@@ -17,9 +17,10 @@
 //  * The step is branch-free: per-half read pointers are SGPRs, the reader
 //    index is v_mbcnt over the ballot, the ring read is unconditional and
 //    the state update one v_perm.
-//  * Compressed words are staged in a 256-word LDS ring per block stream,
-//    refilled 128 words at a time (one u32 per lane) from registers
-//    prefetched at the previous refill.
+//  * Compressed words are staged in a 512-word LDS ring per block stream,
+//    refilled 256 words at a time (8 B per lane) from registers prefetched
+//    at the previous refill; the initial fill holds a typical bf16 block's
+//    whole stream.
 //  * 8-step segments are unrolled (constant LDS offsets); each lane joins 8
 //    words of the segment with their raw float bytes (loaded a segment
 //    earlier) and writes them with 16 B stores.
@@ -61,8 +62,9 @@ __device__ uint64_t g_dbgT[16384 * 24];
 namespace dec {
 constexpr int kThreads = 256;
 constexpr int kWaves = kThreads / 64;
-constexpr uint32_t kRing = 256;      // u16 words per block-stream ring
-constexpr uint32_t kRefill = 128;    // words per refill (64 lanes x 4 B)
+constexpr uint32_t kRing = 512;      // u16 words per block-stream ring
+constexpr uint32_t kRefill = 256;    // words per refill (64 lanes x 8 B)
+constexpr uint32_t kWPL = kRefill / 64;  // words per lane per refill
 constexpr uint32_t kSegSteps = 8;    // decode steps per output segment
 constexpr uint32_t kSegWords = kSegSteps * 32;
 constexpr uint32_t kUnroll = 4;      // steps between ring checks
@@ -97,35 +99,35 @@ struct DStream {
   int32_t ptr[2];               // per half: next read is below ptr
   int32_t lo[2];                // per half: ring holds stream words >= lo
   gp<const uint16_t> data[2];   // per half: block's compressed words (HBM)
-  uint32_t pf[2];               // per half: prefetched words [lo - 128, lo)
+  u32x2 pf[2];                  // per half: prefetched words [lo - 256, lo)
 };
 
-// 2 compressed words at p (4 B load when aligned)
-__device__ __forceinline__ uint32_t ld2w(gp<const uint16_t> p, bool vec) {
-  if (vec) return *(gp<const uint32_t>)p;
-  return uint32_t(p[0]) | (uint32_t(p[1]) << 16);
+// 4 compressed words at p (one 8 B load when aligned)
+__device__ __forceinline__ u32x2 ld4w(gp<const uint16_t> p, bool vec) {
+  if (vec) return *(gp<const u32x2>)p;
+  return u32x2{uint32_t(p[0]) | (uint32_t(p[1]) << 16), uint32_t(p[2]) | (uint32_t(p[3]) << 16)};
 }
 
-// Prefetch words [max(0, lo - 128), lo) of one half (lane j: 2 words).
-// May read one word past lo: inside the block's 8-word padding.
+// Prefetch words [max(0, lo - 256), lo) of one half (lane j: 4 words).  lo
+// stays a multiple of 4, so the lanes cover the range exactly.
 __device__ __forceinline__ void ringPrefetch(DStream& p, int hh, uint32_t lane, bool vec) {
   const int32_t nlo = max(0, p.lo[hh] - int32_t(dec::kRefill));
-  if (p.lo[hh] > 0 && int32_t(2 * lane) < p.lo[hh] - nlo)
-    p.pf[hh] = ld2w(p.data[hh] + nlo + 2 * lane, vec);
+  if (p.lo[hh] > 0 && int32_t(dec::kWPL * lane) < p.lo[hh] - nlo)
+    p.pf[hh] = ld4w(p.data[hh] + nlo + dec::kWPL * lane, vec);
 }
 
 // Before kUnroll steps: if fewer than 32 * kUnroll words are buffered below
-// ptr, refill [lo - 128, lo) from the prefetch registers (the refill
-// overwrites words >= lo + 128, all consumed since ptr < lo + 128) and
-// prefetch the next 128 words.
+// ptr, refill [lo - 256, lo) from the prefetch registers (the refill
+// overwrites words >= lo + 256, all consumed since ptr < lo + 256) and
+// prefetch the next 256 words.
 __device__ __forceinline__ void ringEnsure(DStream& p, uint32_t lane, bool vec) {
   if (DG_EXP == 3 || DG_EXP == 15) return;  // experiment: no refills
 #pragma unroll
   for (int hh = 0; hh < 2; ++hh) {
     if (p.lo[hh] > 0 && p.ptr[hh] - int32_t(32 * dec::kUnroll) < p.lo[hh]) {
       const int32_t nlo = max(0, p.lo[hh] - int32_t(dec::kRefill));
-      if (int32_t(2 * lane) < p.lo[hh] - nlo)
-        *(lp<uint32_t>)(p.ring + hh * dec::kRing + ((nlo + 2 * lane) & (dec::kRing - 1))) = p.pf[hh];
+      if (int32_t(dec::kWPL * lane) < p.lo[hh] - nlo)
+        *(lp<u32x2>)(p.ring + hh * dec::kRing + ((nlo + dec::kWPL * lane) & (dec::kRing - 1))) = p.pf[hh];
       p.lo[hh] = nlo;
       ringPrefetch(p, hh, lane, vec);
     }
@@ -436,7 +438,7 @@ __global__ __launch_bounds__(dec::kThreads) void k_decode(BatchDesc in, BatchDes
           d.ptr[hh] = 0;
           d.lo[hh] = 0;
           d.data[hh] = data;
-          d.pf[hh] = 0;
+          d.pf[hh] = u32x2{0, 0};
           if (bk < nBlocks) {
             const uint2 e = ld8(bw + bk);
             const uint32_t ex = readfirst(e.x), ey = readfirst(e.y);  // wave-uniform: SGPRs
@@ -444,15 +446,17 @@ __global__ __launch_bounds__(dec::kThreads) void k_decode(BatchDesc in, BatchDes
             const int32_t cw = int32_t(ex & 0xffffu);
             d.ptr[hh] = cw;
             d.data[hh] = data + ey;
-            const int32_t lo = cw > int32_t(dec::kRing) ? int32_t(roundUp(uint32_t(cw) - dec::kRing, 2)) : 0;
+            const int32_t lo =
+                cw > int32_t(dec::kRing) ? int32_t(roundUp(uint32_t(cw) - dec::kRing, dec::kWPL)) : 0;
             d.lo[hh] = lo;
-            // initial fill of [lo, cw) (<= 256 words: two wave-wide passes)
+            // initial fill of [lo, cw) (<= 512 words: two wave-wide passes).
+            // The last lane may copy up to 3 words past cw (the block's
+            // 8-word padding) into slots below lo + 512: never a live slot.
 #pragma unroll
-            for (int q = 0; q < 2; ++q) {
-              const int32_t a = lo + q * int32_t(dec::kRefill) + int32_t(2 * lane);
+            for (int q = 0; q < int(dec::kRing / dec::kRefill); ++q) {
+              const int32_t a = lo + q * int32_t(dec::kRefill) + int32_t(dec::kWPL * lane);
               if (a < cw)
-                *(lp<uint32_t>)(d.ring + hh * dec::kRing + (a & (dec::kRing - 1))) =
-                    ld2w(d.data[hh] + a, vecIn);
+                *(lp<u32x2>)(d.ring + hh * dec::kRing + (a & (dec::kRing - 1))) = ld4w(d.data[hh] + a, vecIn);
             }
             ringPrefetch(d, hh, lane, vecIn);
           }
