@@ -173,7 +173,7 @@ def main():
         ach = algo[dominant] / (fam[dominant]["avg_ms"] * 1e-3) / 1e9
         roofline = {"bound": "hbm", "kernel": f"k_{dominant}", "achieved": round(ach, 1),
                     "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBPS, 4),
-                    "traffic": _pmc_traffic(dominant, U, comp_bytes),
+                    "traffic": _pmc_traffic(dominant, ft),
                     "algorithmic_bytes_per_launch": algo[dominant]}
     t_enc = sum(fam[k]["avg_ms"] for k in ("hist", "normalize", "encode", "coalesce") if k in fam)
     t_dec = fam.get("decode", {}).get("avg_ms", 0.0)
@@ -329,9 +329,10 @@ def _extras(dev, pb, reps=3):
     return out
 
 
-def _pmc_traffic(kernel, U, comp):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC
-    summary (profiles/*pmc*.json, written by tools/pmc_summary.py), or None."""
+def _pmc_traffic(kernel, ft):
+    """HBM bytes per launch of `kernel`'s instance for float type `ft` from
+    the newest committed rocprofv3 PMC summary (profiles/*pmc*.json, written
+    by tools/pmc_summary.py, keyed per template instance), or None."""
     def natural(f):  # r01_v10 after r01_v9
         return [int(t) if t.isdigit() else t for t in re.split(r"(\d+)", os.path.basename(f))]
 
@@ -341,9 +342,9 @@ def _pmc_traffic(kernel, U, comp):
             d = json.load(open(f))
         except Exception:
             continue
-        k = d.get("kernels", {}).get("k_" + kernel)
-        if k and "hbm_bytes_per_launch" in k:
-            return k["hbm_bytes_per_launch"]
+        for name, k in d.get("kernels", {}).items():
+            if name.startswith(f"k_{kernel}<{ft},") and "hbm_bytes_per_launch" in k:
+                return k["hbm_bytes_per_launch"]
     return None
 
 

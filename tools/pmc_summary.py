@@ -22,8 +22,13 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def family(name):
-    m = re.search(r"dietgpu::(k_\w+)", name)
-    return m.group(1) if m else None
+    """'void dietgpu::k_decode<2, 0>(...)' -> 'k_decode<2,0>': one entry per
+    template instance, so the bf16 launches are not averaged with the byte
+    (c3) or fp64 launches of the bench's secondary configs."""
+    m = re.search(r"dietgpu::(?:\(anonymous namespace\)::)?(k_\w+)(<[^>(]*>)?", name)
+    if not m:
+        return None
+    return m.group(1) + (m.group(2) or "").replace(" ", "")
 
 
 def main(src, tag):
