@@ -107,7 +107,7 @@ def main():
         assert torch.equal(out.view(torch.int16), x.view(torch.int16)), "roundtrip mismatch"
     comp_bytes = int(sizes.to(torch.int64).sum().item())
 
-    FAMILIES = ("hist", "normalize", "encode", "coalesce", "decode")
+    FAMILIES = ("compress", "hist", "normalize", "encode", "coalesce", "decode")
 
     def query_families():
         fam = {}
@@ -166,7 +166,7 @@ def main():
 
     # algorithmic bytes per launch (Measurement): one launch covers
     # the whole batch; C = compressed bytes (raw section + ANS), U = input.
-    algo = {"decode": U + comp_bytes, "encode": U + comp_bytes, "hist": U,
+    algo = {"decode": U + comp_bytes, "encode": U + comp_bytes, "compress": U + comp_bytes, "hist": U,
             "coalesce": 2 * max(comp_bytes - U // 2, 0), "normalize": 0}
     roofline = None
     if dominant:
@@ -175,7 +175,7 @@ def main():
                     "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBPS, 4),
                     "traffic": _pmc_traffic(dominant, ft),
                     "algorithmic_bytes_per_launch": algo[dominant]}
-    t_enc = sum(fam[k]["avg_ms"] for k in ("hist", "normalize", "encode", "coalesce") if k in fam)
+    t_enc = sum(fam[k]["avg_ms"] for k in ("compress", "hist", "normalize", "encode", "coalesce") if k in fam)
     t_dec = fam.get("decode", {}).get("avg_ms", 0.0)
     line = {
         "metric": METRIC, "value": round(value, 2), "unit": "GB/s", "n_gpus": world,
@@ -236,7 +236,7 @@ def _extras(dev, pb, reps=3):
 
     out = []
 
-    fams = ("hist", "normalize", "encode", "coalesce", "decode", "sparse")
+    fams = ("compress", "hist", "normalize", "encode", "coalesce", "decode", "sparse")
 
     def breakdown(fc, fd):
         """avg ms per launch of each kernel family in one extra profiled call

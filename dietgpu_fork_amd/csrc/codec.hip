@@ -19,6 +19,7 @@
 #include "codec_internal.h"
 #include "dietgpu/GpuANSCodec.h"
 #include "dietgpu/GpuFloatCodec.h"
+#include "compress.h"
 #include "decode.h"
 #include "encode.h"
 #include "profile.h"
@@ -54,6 +55,62 @@ void checkProbBits(int pb) {
 // ---------------------------------------------------------------------------
 // generic drivers
 // ---------------------------------------------------------------------------
+// Single-pass compression (k_compress, compress.h) for single-segment formats
+// without a caller-supplied histogram.  A team (the workgroups of one element)
+// meets at a barrier, so it must fit on the device with room to spare: at most
+// half the resident slots (each XCD then holds its ceil(team / 8) share).
+template <int FT, bool kCk>
+bool compressSinglePass(StackDeviceMemory& res, int pb, bool useChecksum, uint32_t nb,
+                        const BatchDesc& in, uint32_t maxSize, const BatchDesc& out,
+                        uint32_t* outSize_dev, hipStream_t s) {
+  const uint32_t MB = divUp(maxSize, kBlockSize);
+  const uint32_t nW = std::max(1u, divUp(MB, cmp::kBlocksPerWG));
+  static uint32_t slots = 0;
+  if (slots == 0)
+    slots = residentSlots(reinterpret_cast<const void*>(&k_compress<FT, kCk>), cmp::kThreads, 0);
+  if (DG_EXP == 40 || nW > cmp::kMaxTeam || uint64_t(nW) * 2 > slots) return false;
+
+  auto part = res.alloc<uint32_t>(s, size_t(nb) * nW * kNumSymbols);
+  auto partCk = res.alloc<uint32_t>(s, kCk ? size_t(nb) * nW : 1);
+  // one zeroed region: look-back flags, then the per-element sync records
+  const size_t flagBytes = roundUp64(uint64_t(nb) * nW * 8, 256);
+  const size_t syncBytes = size_t(nb) * cmp::kSyncWords * 4;
+  auto zeroed = res.alloc<uint8_t>(s, flagBytes + syncBytes);
+  auto slotMem = res.alloc<uint8_t>(s, size_t(nb) * std::max(MB, 1u) * kSlotDataBytes);
+  auto ck = res.alloc<uint32_t>(s, FT != 0 && useChecksum ? nb : 1);
+  HIP_CHECK(hipMemsetAsync(zeroed.data(), 0, flagBytes + syncBytes, s));
+  if (FT != 0 && useChecksum) {
+    HIP_CHECK(hipMemsetAsync(ck.data(), 0, sizeof(uint32_t) * nb, s));
+  }
+  CompScratch sc;
+  sc.part = part.data();
+  sc.partCk = partCk.data();
+  sc.flags = reinterpret_cast<uint64_t*>(zeroed.data());
+  sc.sync = reinterpret_cast<uint32_t*>(zeroed.data() + flagBytes);
+  sc.slots = slotMem.data();
+  sc.ckIn = FT != 0 && useChecksum ? ck.data() : nullptr;
+  sc.outSize = outSize_dev;
+  sc.nW = nW;
+  sc.MB = std::max(MB, 1u);
+  sc.pb = pb;
+  sc.useChecksum = useChecksum;
+  for (uint32_t y0 = 0; y0 < nb; y0 += kMaxGridY) {
+    const uint32_t ny = std::min(kMaxGridY, nb - y0);
+    if (FT != 0 && useChecksum) {
+      // float checksum: the reference passes float-word counts as byte counts
+      // (float/GpuFloatCompress.cuh:709)
+      const uint32_t ckChunk = 1u << 20;
+      dim3 g(std::max(1u, divUp(maxSize, ckChunk)), ny);
+      k_checksum<<<g, kThreads, 0, s>>>(in, y0, 1, ckChunk, ck.data());
+      HIP_LAUNCH_CHECK();
+    }
+    prof::Scope p("compress", s);
+    k_compress<FT, kCk><<<dim3(nW, ny), cmp::kThreads, 0, s>>>(in, out, y0, sc);
+    HIP_LAUNCH_CHECK();
+  }
+  return true;
+}
+
 template <int FT>
 void encodeBatchDevice(StackDeviceMemory& res, int pb, bool useChecksum, uint32_t nb,
                        const BatchDesc& in, uint32_t maxSize, const uint32_t* hist_dev,
@@ -68,6 +125,15 @@ void encodeBatchDevice(StackDeviceMemory& res, int pb, bool useChecksum, uint32_
   const bool userHist = FT == 0 && hist_dev != nullptr;
   const bool runHist = !userHist || useChecksum;
   const bool rawCk = FT == 0 && useChecksum;
+  if constexpr (kFused) {
+    if (!userHist) {
+      const bool done = rawCk ? compressSinglePass<FT, FT == 0>(res, pb, useChecksum, nb, in, maxSize,
+                                                                 out, outSize_dev, s)
+                              : compressSinglePass<FT, false>(res, pb, useChecksum, nb, in, maxSize,
+                                                              out, outSize_dev, s);
+      if (done) return;
+    }
+  }
 
   auto partHist = res.alloc<uint32_t>(s, runHist ? size_t(kSegs) * nb * chunks * kNumSymbols : 1);
   auto partCk = res.alloc<uint32_t>(s, rawCk ? size_t(nb) * chunks : 1);

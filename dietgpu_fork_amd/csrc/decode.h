@@ -35,29 +35,7 @@
 #endif
 
 namespace dietgpu {
-#if DG_EXP == 7 || defined(DG_TRACE)
-// experiment 7: per-wave s_memtime stamps (lane 0), 24 slots per wave
-__device__ uint64_t g_dbgT[16384 * 24];
-#define DG_STAMP(slot)                                                                \
-  do {                                                                                \
-    if (lane == 0 && blockIdx.y * gridDim.x * 4 < 16384)                              \
-      g_dbgT[((blockIdx.y * gridDim.x + blockIdx.x) * 4 + w) * 24 + (slot)] =         \
-          __builtin_amdgcn_s_memtime();                                               \
-  } while (0)
-#define DG_STAMP_RT(slot)                                                             \
-  do {                                                                                \
-    if (lane == 0 && blockIdx.y * gridDim.x * 4 < 16384)                              \
-      g_dbgT[((blockIdx.y * gridDim.x + blockIdx.x) * 4 + w) * 24 + (slot)] =         \
-          __builtin_amdgcn_s_memrealtime();                                           \
-  } while (0)
-#else
-#define DG_STAMP(slot) \
-  do {                 \
-  } while (0)
-#define DG_STAMP_RT(slot) \
-  do {                    \
-  } while (0)
-#endif
+// per-wave trace stamps (DG_STAMP / DG_STAMP_RT): device.h
 
 namespace dec {
 constexpr int kThreads = 256;

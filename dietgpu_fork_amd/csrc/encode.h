@@ -189,17 +189,72 @@ static __global__ __launch_bounds__(kThreads) void k_histReduce(
   }
 }
 
-// ---------------------------------------------------------------------------
-// k_normalize: one workgroup per (element, segment).  Bit-exact restatement of
-// normalizeProbabilitiesFromHistogram (ans/GpuANSStatistics.cuh:178-366):
-// float32 quantisation, descending order of the unique keys (q << 16) | sym
-// by rank counting (in place of cub::BlockRadixSort), the diff > 0 bump of
-// *symbol ids* < diff, the diff < 0 decrement of sorted ranks [g-k, g), and
-// the exclusive cdf.  Encode table entry (internal, never archived):
+// Bit-exact restatement of normalizeProbabilitiesFromHistogram
+// (ans/GpuANSStatistics.cuh:178-366) for one kThreads-thread workgroup, thread
+// s = symbol s: float32 quantisation, descending order of the unique keys
+// (q << 16) | sym by rank counting (in place of cub::BlockRadixSort), the
+// diff > 0 bump of *symbol ids* < diff, and the diff < 0 decrement of sorted
+// ranks [g-k, g).  Returns this symbol's pdf.  total > 0; whole workgroup.
+__device__ __forceinline__ uint32_t normalizeCount(uint32_t count, uint32_t total, int pb,
+                                                   uint32_t* keys, uint32_t* red) {
+  const uint32_t s = threadIdx.x;
+  const uint32_t W = 1u << pb;
+  const float r = __fdiv_rn(float(count), float(total));
+  const float f = __fmul_rn(float(W), r);
+  uint32_t q = uint32_t(f);
+  if (count > 0 && q == 0) q = 1;
+  const uint32_t qsum = blockSum<kThreads>(q, red);
+
+  const int diff = int(W) - int(qsum);
+  uint32_t rank = kNumSymbols;
+  if (diff < 0) {
+    // Only entries with q > 1 are ever decremented, and they form a prefix
+    // [0, g) of the descending key order, so a symbol's rank among the
+    // (typically ~20) keys with q > 1 equals its rank in the full sort.
+    const uint32_t key = (q << 16) | s;
+    uint32_t g0;
+    const uint32_t pos = blockExclusiveScan<kThreads>(q > 1 ? 1u : 0u, red, &g0);
+    if (q > 1) keys[pos] = key;
+    __syncthreads();
+    if (q > 1) {
+      rank = 0;
+      for (uint32_t t = 0; t < g0; ++t) rank += keys[t] > key ? 1u : 0u;
+    }
+  }
+  if (diff > 0) {
+    q += uint32_t(diff) / kNumSymbols + (s < uint32_t(diff) % kNumSymbols ? 1u : 0u);
+  } else if (diff < 0) {
+    int d = -diff;
+    while (d > 0) {
+      const int g = int(blockSum<kThreads>(q > 1 ? 1u : 0u, red));
+      if (g == 0) break;  // reference asserts; unreachable for real tables
+      const int k = d < g ? d : g;
+      if (int(rank) >= g - k && int(rank) < g) q -= 1;
+      d -= k;
+    }
+  }
+  return q;
+}
+
+// Encode table entry (internal, never archived) of a symbol with pdf q and
+// cumulative frequency cdf:
 //   x = pdf << (31 - pb)              renormalisation threshold
 //   y = magic                         x / pdf == (umulhi(x, magic) + x) >> shift
 //   z = cdf
 //   w = (2^pb - pdf) | shift << 24    x' = x + cdf + (x / pdf) * (2^pb - pdf)
+__device__ __forceinline__ uint4 encTableEntry(uint32_t q, uint32_t cdf, int pb) {
+  uint32_t shift = 0, magic = 0;
+  if (q > 0) {
+    shift = 32 - __clz(q - 1);
+    magic = uint32_t(((1ull << 32) * ((1ull << shift) - q)) / q + 1);
+  }
+  return make_uint4(q << (kStateBits - pb), magic, cdf, ((1u << pb) - q) | (shift << 24));
+}
+
+// ---------------------------------------------------------------------------
+// k_normalize: one workgroup per (element, segment): sums the partial
+// histograms, normalises (normalizeCount) and stores the encode table rows
+// (encTableEntry) and the u16 pdf.
 // ---------------------------------------------------------------------------
 static __global__ __launch_bounds__(kThreads) void k_normalize(
     BatchDesc in, uint32_t batchOffset, uint32_t numInBatch, const uint32_t* __restrict__ hist,
@@ -231,41 +286,9 @@ static __global__ __launch_bounds__(kThreads) void k_normalize(
     G(pdfOut)[row * kNumSymbols + s] = 0;
     return;
   }
-  const uint32_t W = 1u << pb;
-  const float r = __fdiv_rn(float(count), float(total));
-  const float f = __fmul_rn(float(W), r);
-  uint32_t q = uint32_t(f);
-  if (count > 0 && q == 0) q = 1;
-  const uint32_t qsum = blockSum<kThreads>(q, red);
-
-  const uint32_t key = (q << 16) | s;
-  keys[s] = key;
-  __syncthreads();
-  uint32_t rank = 0;
-#pragma unroll 8
-  for (uint32_t t = 0; t < kNumSymbols; ++t) rank += keys[t] > key ? 1u : 0u;
-
-  const int diff = int(W) - int(qsum);
-  if (diff > 0) {
-    q += uint32_t(diff) / kNumSymbols + (s < uint32_t(diff) % kNumSymbols ? 1u : 0u);
-  } else if (diff < 0) {
-    int d = -diff;
-    while (d > 0) {
-      const int g = int(blockSum<kThreads>(q > 1 ? 1u : 0u, red));
-      if (g == 0) break;  // reference asserts; unreachable for real tables
-      const int k = d < g ? d : g;
-      if (int(rank) >= g - k && int(rank) < g) q -= 1;
-      d -= k;
-    }
-  }
+  const uint32_t q = normalizeCount(count, total, pb, keys, red);
   const uint32_t cdf = blockExclusiveScan<kThreads>(q, red, nullptr);
-  uint32_t shift = 0, magic = 0;
-  if (q > 0) {
-    shift = 32 - __clz(q - 1);
-    magic = uint32_t(((1ull << 32) * ((1ull << shift) - q)) / q + 1);
-  }
-  st16(G(table) + row * kNumSymbols + s,
-       make_uint4(q << (kStateBits - pb), magic, cdf, (W - q) | (shift << 24)));
+  st16(G(table) + row * kNumSymbols + s, encTableEntry(q, cdf, pb));
   G(pdfOut)[row * kNumSymbols + s] = uint16_t(q);
 }
 
@@ -325,13 +348,13 @@ struct EStream {
 // issued, so waits for those loads never drain fresh stores) and with
 // kAt = 384 every kUnroll steps (only dense data gets there; it keeps the
 // ring from overflowing: pending <= 383 + 128 < 512).
-template <int kAt>
+template <int kAt, uint32_t kRing = enc::kRing>
 __device__ __forceinline__ void ringFlush(EStream& p, uint32_t lane) {
 #pragma unroll
   for (int hh = 0; hh < 2; ++hh) {
     if (p.nout[hh] - p.flushed[hh] >= kAt) {
       const int32_t a = p.flushed[hh] + int32_t(4 * lane);
-      *(gp<u32x2>)(p.out[hh] + a) = *(lp<const u32x2>)(p.ring + hh * enc::kRing + (a & (enc::kRing - 1)));
+      *(gp<u32x2>)(p.out[hh] + a) = *(lp<const u32x2>)(p.ring + hh * kRing + (a & (kRing - 1)));
       p.flushed[hh] += enc::kFlush;
     }
   }
@@ -354,7 +377,7 @@ __device__ __forceinline__ void ringFlushAll(EStream& p, uint32_t lane) {
 // stream of a block pair, given the symbol's table entry e; writers emit in
 // ascending lane order.  hv: all-ones on lanes 32-63 (opaque to the
 // compiler).  Masked (!valid) lanes neither write nor change state.
-template <bool kMask>
+template <bool kMask, uint32_t kRing = enc::kRing>
 __device__ __forceinline__ void encStep(EStream& p, bool valid, const u32x4& e, uint32_t hv,
                                         uint32_t trashAddr) {
   const bool wr = kMask ? (valid && p.x >= e.x) : (p.x >= e.x);
@@ -369,7 +392,7 @@ __device__ __forceinline__ void encStep(EStream& p, bool valid, const u32x4& e, 
   p.nout[1] += cHi;
   const uint32_t idx = __builtin_amdgcn_mbcnt_hi(uint32_t(vote >> 32),
                                                  __builtin_amdgcn_mbcnt_lo(uint32_t(vote), vbase));
-  const uint32_t ringAddr = uint32_t(size_t(p.ringLane + (idx & (enc::kRing - 1))));
+  const uint32_t ringAddr = uint32_t(size_t(p.ringLane + (idx & (kRing - 1))));
   // non-writers store to their trash dword: one v_cndmask on the ballot mask
   // and an unconditional ds_write, no exec-mask split of the step
   uint32_t dst;
