@@ -13,6 +13,16 @@
 
 namespace dietgpu {
 
+// Per-call pointer / size / offset tables small enough to ride in the kernel
+// arguments of the hot kernels (k_compress, k_decode): the reference inlines
+// up to 128 pointers in its kernel parameters (BatchProviderInlinePointer,
+// ans/BatchProvider.cuh:100-194); here up to 8 KB of table (about 400
+// elements), so a pointer-API call launches no upload kernel at all.
+constexpr uint32_t kInlineWords = 1024;
+struct InlineTable {
+  uint64_t w[kInlineWords];
+};
+
 struct BatchDesc {
   enum : uint32_t { kStride = 0, kPointer = 1, kSplit = 2 };
   uint32_t mode = kStride;
@@ -22,14 +32,56 @@ struct BatchDesc {
   const uint64_t* ptrs = nullptr;    // pointer mode: device array of addresses
   const uint32_t* sizes = nullptr;   // per-element sizes (units), optional
   const uint64_t* offsets = nullptr; // split mode: byte offset of element b
+  // fields whose value is a byte offset into the launch's InlineTable
+  enum : uint32_t { kInlPtrs = 1, kInlSizes = 2, kInlOffsets = 4 };
+  uint32_t inl = 0;
+
+  // A field flagged in `inl` holds a byte offset into the launch's
+  // InlineTable, which must be the kernel's FIRST parameter: it is read in
+  // place at the start of the kernarg segment (naming the parameter would
+  // make the compiler copy all 8 KB into scratch).  Resolved at each use
+  // (uniform scalar arithmetic), so the descriptor stays in the kernarg
+  // segment and occupies no registers.
+  // Element b's entry of an inline field (b uniform): a scalar-uniform read
+  // of the kernarg segment (readfirstlane keeps every value derived from it
+  // in SGPRs, as with a plain descriptor).
+  template <typename T>
+  __device__ __forceinline__ T inlineAt(const void* field, uint32_t b) const {
+#if defined(__HIP_DEVICE_COMPILE__)  // (the host pass only parses device code)
+    const T* p = reinterpret_cast<const T*>((const uint8_t*)__builtin_amdgcn_kernarg_segment_ptr() +
+                                            reinterpret_cast<uintptr_t>(field));
+    const T v = p[b];
+    if constexpr (sizeof(T) == 8) {
+      const uint64_t u = uint64_t(v);
+      // (the builtin returns int: widen through uint32_t, never sign-extend)
+      const uint32_t lo = uint32_t(__builtin_amdgcn_readfirstlane(uint32_t(u)));
+      const uint32_t hi = uint32_t(__builtin_amdgcn_readfirstlane(uint32_t(u >> 32)));
+      return T(uint64_t(lo) | (uint64_t(hi) << 32));
+    } else {
+      return T(uint32_t(__builtin_amdgcn_readfirstlane(uint32_t(v))));
+    }
+#else
+    (void)field;
+    (void)b;
+    return T(0);
+#endif
+  }
 
   __device__ __forceinline__ uint8_t* start(uint32_t b) const {
-    if (mode == kPointer) return reinterpret_cast<uint8_t*>(ptrs[b]);
-    if (mode == kSplit) return base + offsets[b];
+    if (mode == kPointer) {
+      if (inl & kInlPtrs) return reinterpret_cast<uint8_t*>(inlineAt<uint64_t>(ptrs, b));
+      return reinterpret_cast<uint8_t*>(ptrs[b]);
+    }
+    if (mode == kSplit) {
+      if (inl & kInlOffsets) return base + inlineAt<uint64_t>(offsets, b);
+      return base + offsets[b];
+    }
     return base + stride * b;
   }
   __device__ __forceinline__ uint32_t size(uint32_t b) const {
-    return sizes ? sizes[b] : fixedSize;
+    if (!sizes) return fixedSize;
+    if (inl & kInlSizes) return inlineAt<uint32_t>(sizes, b);
+    return sizes[b];
   }
 
   static BatchDesc strided(const void* p, uint64_t strideBytes, uint32_t size) {

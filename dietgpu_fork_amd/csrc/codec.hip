@@ -10,6 +10,7 @@
 //   decompress: k_decode (table build + rANS decode + float join fused)
 #include <algorithm>
 #include <cstring>
+#include <memory>
 #include <sstream>
 #include <vector>
 
@@ -53,6 +54,89 @@ void checkProbBits(int pb) {
 }  // namespace
 
 // ---------------------------------------------------------------------------
+// parameter tables (the reference's BatchProvider pointer / size arrays)
+// ---------------------------------------------------------------------------
+// Small tables (allowInline, <= 8 KB) ride in the InlineTable kernel argument
+// of k_compress / k_decode: the BatchDesc fields then hold byte offsets into
+// it (biased by 8, so none is 0) and BatchDesc::inl says which.  Any other
+// kernel gets a device copy made in its driver's scope (DeviceDescs).  Larger
+// tables, or callers that need device pointers, get one upload here.
+struct DeviceTables {
+  GpuMemoryReservation<uint8_t> mem;
+  std::vector<uint8_t> host;
+  std::unique_ptr<InlineTable> image;  // kernarg image when inline
+  bool inl = false;
+  const uint64_t* u64a = nullptr;
+  const uint64_t* u64b = nullptr;
+  const uint32_t* u32a = nullptr;
+
+  // mark the table-backed fields of a descriptor built from u64a/u64b/u32a
+  BatchDesc tag(BatchDesc d) const {
+    if (!inl) return d;
+    if (d.ptrs) d.inl |= BatchDesc::kInlPtrs;
+    if (d.sizes) d.inl |= BatchDesc::kInlSizes;
+    if (d.offsets) d.inl |= BatchDesc::kInlOffsets;
+    return d;
+  }
+};
+constexpr size_t kInlineBias = 8;
+
+const InlineTable& kernargTable(const DeviceTables* t) {
+  static const InlineTable kEmpty{};
+  return t && t->inl ? *t->image : kEmpty;
+}
+
+DeviceTables uploadTables(StackDeviceMemory& res, hipStream_t s, uint32_t nb,
+                          const std::vector<uint64_t>& a, const std::vector<uint64_t>& b,
+                          const std::vector<uint32_t>& c, bool allowInline = false) {
+  const size_t bytesA = a.size() * 8, bytesB = b.size() * 8, bytesC = c.size() * 4;
+  DeviceTables t;
+  t.host.resize(bytesA + bytesB + bytesC);
+  if (bytesA) std::memcpy(t.host.data(), a.data(), bytesA);
+  if (bytesB) std::memcpy(t.host.data() + bytesA, b.data(), bytesB);
+  if (bytesC) std::memcpy(t.host.data() + bytesA + bytesB, c.data(), bytesC);
+  t.inl = allowInline && kInlineBias + t.host.size() <= sizeof(InlineTable);
+  uintptr_t base;
+  if (t.inl) {
+    t.image.reset(new InlineTable());
+    std::memcpy(reinterpret_cast<uint8_t*>(t.image->w) + kInlineBias, t.host.data(), t.host.size());
+    base = kInlineBias;
+  } else {
+    t.mem = res.alloc<uint8_t>(s, std::max<size_t>(t.host.size(), 1));
+    StackDeviceMemory::copyToDevice(t.mem.data(), t.host.data(), t.host.size(), s);
+    base = reinterpret_cast<uintptr_t>(t.mem.data());
+  }
+  t.u64a = reinterpret_cast<const uint64_t*>(base);
+  t.u64b = reinterpret_cast<const uint64_t*>(base + bytesA);
+  t.u32a = reinterpret_cast<const uint32_t*>(base + bytesA + bytesB);
+  (void)nb;
+  return t;
+}
+
+// Device copy of inline tables for kernels without an InlineTable argument,
+// allocated in the calling driver's scope (the arena is LIFO) and only when
+// the tables are inline.
+struct DeviceDescs {
+  GpuMemoryReservation<uint8_t> mem;
+  uintptr_t base = 0;
+  DeviceDescs(StackDeviceMemory& res, hipStream_t s, const DeviceTables* t) {
+    if (!t || !t->inl) return;
+    mem = res.alloc<uint8_t>(s, std::max<size_t>(t->host.size(), 1));
+    StackDeviceMemory::copyToDevice(mem.data(), t->host.data(), t->host.size(), s);
+    base = reinterpret_cast<uintptr_t>(mem.data()) - kInlineBias;
+  }
+  BatchDesc map(BatchDesc d) const {
+    if (!d.inl) return d;
+    auto rebase = [&](auto p) { return reinterpret_cast<decltype(p)>(base + reinterpret_cast<uintptr_t>(p)); };
+    if (d.inl & BatchDesc::kInlPtrs) d.ptrs = rebase(d.ptrs);
+    if (d.inl & BatchDesc::kInlSizes) d.sizes = rebase(d.sizes);
+    if (d.inl & BatchDesc::kInlOffsets) d.offsets = rebase(d.offsets);
+    d.inl = 0;
+    return d;
+  }
+};
+
+// ---------------------------------------------------------------------------
 // generic drivers
 // ---------------------------------------------------------------------------
 // Single-pass compression (k_compress, compress.h) for single-segment formats
@@ -62,7 +146,7 @@ void checkProbBits(int pb) {
 template <int FT, bool kCk>
 bool compressSinglePass(StackDeviceMemory& res, int pb, bool useChecksum, uint32_t nb,
                         const BatchDesc& in, uint32_t maxSize, const BatchDesc& out,
-                        uint32_t* outSize_dev, hipStream_t s) {
+                        uint32_t* outSize_dev, hipStream_t s, const DeviceTables* tabs) {
   const uint32_t MB = divUp(maxSize, kBlockSize);
   const uint32_t nW = std::max(1u, divUp(MB, cmp::kBlocksPerWG));
   static uint32_t slots = 0;
@@ -78,6 +162,7 @@ bool compressSinglePass(StackDeviceMemory& res, int pb, bool useChecksum, uint32
   auto zeroed = res.alloc<uint8_t>(s, flagBytes + syncBytes);
   auto slotMem = res.alloc<uint8_t>(s, size_t(nb) * std::max(MB, 1u) * kSlotDataBytes);
   auto ck = res.alloc<uint32_t>(s, FT != 0 && useChecksum ? nb : 1);
+  DeviceDescs dd(res, s, FT != 0 && useChecksum ? tabs : nullptr);  // k_checksum's view
   HIP_CHECK(hipMemsetAsync(zeroed.data(), 0, flagBytes + syncBytes, s));
   if (FT != 0 && useChecksum) {
     HIP_CHECK(hipMemsetAsync(ck.data(), 0, sizeof(uint32_t) * nb, s));
@@ -101,11 +186,11 @@ bool compressSinglePass(StackDeviceMemory& res, int pb, bool useChecksum, uint32
       // (float/GpuFloatCompress.cuh:709)
       const uint32_t ckChunk = 1u << 20;
       dim3 g(std::max(1u, divUp(maxSize, ckChunk)), ny);
-      k_checksum<<<g, kThreads, 0, s>>>(in, y0, 1, ckChunk, ck.data());
+      k_checksum<<<g, kThreads, 0, s>>>(dd.map(in), y0, 1, ckChunk, ck.data());
       HIP_LAUNCH_CHECK();
     }
     prof::Scope p("compress", s);
-    k_compress<FT, kCk><<<dim3(nW, ny), cmp::kThreads, 0, s>>>(in, out, y0, sc);
+    k_compress<FT, kCk><<<dim3(nW, ny), cmp::kThreads, 0, s>>>(kernargTable(tabs), in, out, y0, sc);
     HIP_LAUNCH_CHECK();
   }
   return true;
@@ -113,8 +198,9 @@ bool compressSinglePass(StackDeviceMemory& res, int pb, bool useChecksum, uint32
 
 template <int FT>
 void encodeBatchDevice(StackDeviceMemory& res, int pb, bool useChecksum, uint32_t nb,
-                       const BatchDesc& in, uint32_t maxSize, const uint32_t* hist_dev,
-                       const BatchDesc& out, uint32_t* outSize_dev, hipStream_t s) {
+                       const BatchDesc& inArg, uint32_t maxSize, const uint32_t* hist_dev,
+                       const BatchDesc& outArg, uint32_t* outSize_dev, hipStream_t s,
+                       const DeviceTables* tabs = nullptr) {
   checkProbBits(pb);
   if (nb == 0) return;
   constexpr int kSegs = FloatTraits<FT>::kSegs;
@@ -127,13 +213,16 @@ void encodeBatchDevice(StackDeviceMemory& res, int pb, bool useChecksum, uint32_
   const bool rawCk = FT == 0 && useChecksum;
   if constexpr (kFused) {
     if (!userHist) {
-      const bool done = rawCk ? compressSinglePass<FT, FT == 0>(res, pb, useChecksum, nb, in, maxSize,
-                                                                 out, outSize_dev, s)
-                              : compressSinglePass<FT, false>(res, pb, useChecksum, nb, in, maxSize,
-                                                              out, outSize_dev, s);
+      const bool done = rawCk ? compressSinglePass<FT, FT == 0>(res, pb, useChecksum, nb, inArg,
+                                                                 maxSize, outArg, outSize_dev, s, tabs)
+                              : compressSinglePass<FT, false>(res, pb, useChecksum, nb, inArg, maxSize,
+                                                              outArg, outSize_dev, s, tabs);
       if (done) return;
     }
   }
+  // three-kernel path: plain device tables
+  DeviceDescs dd(res, s, tabs);
+  const BatchDesc in = dd.map(inArg), out = dd.map(outArg);
 
   auto partHist = res.alloc<uint32_t>(s, runHist ? size_t(kSegs) * nb * chunks * kNumSymbols : 1);
   auto partCk = res.alloc<uint32_t>(s, rawCk ? size_t(nb) * chunks : 1);
@@ -224,7 +313,7 @@ void encodeBatchDevice(StackDeviceMemory& res, int pb, bool useChecksum, uint32_
 template <int FT>
 void decodeBatchDevice(StackDeviceMemory& res, int pb, uint32_t nb, const BatchDesc& in,
                        const BatchDesc& out, uint32_t maxCapacity, uint8_t* outSuccess_dev,
-                       uint32_t* outSize_dev, hipStream_t s) {
+                       uint32_t* outSize_dev, hipStream_t s, const DeviceTables* tabs = nullptr) {
   checkProbBits(pb);
   if (nb == 0) return;
   const uint32_t maxBlocks = divUp(maxCapacity, kBlockSize);
@@ -241,7 +330,8 @@ void decodeBatchDevice(StackDeviceMemory& res, int pb, uint32_t nb, const BatchD
           residentSlots(reinterpret_cast<const void*>(&k_decode<FT, KK>), dec::kThreads, lds);
       const uint32_t P = std::max(1u, uint32_t((uint64_t(chunks) * ny + slots / 2) / slots));
       dim3 g(divUp(chunks, P), ny);
-      k_decode<FT, KK><<<g, dec::kThreads, lds, s>>>(in, out, y0, pb, P, outSuccess_dev, outSize_dev);
+      k_decode<FT, KK><<<g, dec::kThreads, lds, s>>>(kernargTable(tabs), in, out, y0, pb, P,
+                                                     outSuccess_dev, outSize_dev);
       HIP_LAUNCH_CHECK();
     }
   };
@@ -251,11 +341,14 @@ void decodeBatchDevice(StackDeviceMemory& res, int pb, uint32_t nb, const BatchD
 // Verify stored checksums against `unitBytes * out.size(b)` decoded bytes
 // (ansDecodeBatch :557-591 / floatDecompressDevice :1077-1112).  Host sync.
 std::vector<std::pair<int, std::string>> verifyChecksums(StackDeviceMemory& res, uint32_t nb,
-                                                         const BatchDesc& archives, bool isFloat,
-                                                         const BatchDesc& decoded,
-                                                         uint32_t maxBytes, hipStream_t s) {
+                                                         const BatchDesc& archivesArg, bool isFloat,
+                                                         const BatchDesc& decodedArg,
+                                                         uint32_t maxBytes, hipStream_t s,
+                                                         const DeviceTables* tabs) {
   std::vector<std::pair<int, std::string>> errs;
   if (nb == 0) return errs;
+  DeviceDescs dd(res, s, tabs);
+  const BatchDesc archives = dd.map(archivesArg), decoded = dd.map(decodedArg);
   auto now = res.alloc<uint32_t>(s, nb);
   auto old = res.alloc<uint32_t>(s, nb);
   HIP_CHECK(hipMemsetAsync(now.data(), 0, sizeof(uint32_t) * nb, s));
@@ -279,34 +372,6 @@ std::vector<std::pair<int, std::string>> verifyChecksums(StackDeviceMemory& res,
     }
   }
   return errs;
-}
-
-// ---------------------------------------------------------------------------
-// parameter tables (one pinned H2D copy per call)
-// ---------------------------------------------------------------------------
-struct DeviceTables {
-  GpuMemoryReservation<uint8_t> mem;
-  const uint64_t* u64a = nullptr;
-  const uint64_t* u64b = nullptr;
-  const uint32_t* u32a = nullptr;
-};
-
-DeviceTables uploadTables(StackDeviceMemory& res, hipStream_t s, uint32_t nb,
-                          const std::vector<uint64_t>& a, const std::vector<uint64_t>& b,
-                          const std::vector<uint32_t>& c) {
-  const size_t bytesA = a.size() * 8, bytesB = b.size() * 8, bytesC = c.size() * 4;
-  std::vector<uint8_t> host(bytesA + bytesB + bytesC);
-  if (bytesA) std::memcpy(host.data(), a.data(), bytesA);
-  if (bytesB) std::memcpy(host.data() + bytesA, b.data(), bytesB);
-  if (bytesC) std::memcpy(host.data() + bytesA + bytesB, c.data(), bytesC);
-  DeviceTables t;
-  t.mem = res.alloc<uint8_t>(s, std::max<size_t>(host.size(), 1));
-  StackDeviceMemory::copyToDevice(t.mem.data(), host.data(), host.size(), s);
-  t.u64a = reinterpret_cast<const uint64_t*>(t.mem.data());
-  t.u64b = reinterpret_cast<const uint64_t*>(t.mem.data() + bytesA);
-  t.u32a = reinterpret_cast<const uint32_t*>(t.mem.data() + bytesA + bytesB);
-  (void)nb;
-  return t;
 }
 
 static void checkOutAligned(const void* p, const char* what) {
@@ -355,11 +420,11 @@ void ansEncodeBatchPointer(StackDeviceMemory& res, const ANSCodecConfig& config,
     sz[i] = inSize[i];
     maxSize = std::max(maxSize, inSize[i]);
   }
-  auto t = uploadTables(res, stream, numInBatch, ip, op, sz);
-  auto inD = BatchDesc::pointers(t.u64a, t.u32a);
-  auto outD = BatchDesc::pointers(t.u64b, nullptr);
+  auto t = uploadTables(res, stream, numInBatch, ip, op, sz, true);
+  auto inD = t.tag(BatchDesc::pointers(t.u64a, t.u32a));
+  auto outD = t.tag(BatchDesc::pointers(t.u64b, nullptr));
   encodeBatchDevice<0>(res, config.probBits, config.useChecksum, numInBatch, inD, maxSize,
-                       histogram_dev, outD, outSize_dev, stream);
+                       histogram_dev, outD, outSize_dev, stream, &t);
 }
 
 void ansEncodeBatchSplitSize(StackDeviceMemory& res, const ANSCodecConfig& config,
@@ -386,21 +451,21 @@ void ansEncodeBatchSplitSize(StackDeviceMemory& res, const ANSCodecConfig& confi
     run += inSplitSizes[i];
     maxSize = std::max(maxSize, inSplitSizes[i]);
   }
-  auto t = uploadTables(res, stream, numInBatch, off, {}, sz);
-  auto inD = BatchDesc::split(in_dev, t.u64a, t.u32a);
+  auto t = uploadTables(res, stream, numInBatch, off, {}, sz, true);
+  auto inD = t.tag(BatchDesc::split(in_dev, t.u64a, t.u32a));
   auto outD = BatchDesc::strided(out_dev, outStride, 0);
   encodeBatchDevice<0>(res, config.probBits, config.useChecksum, numInBatch, inD, maxSize,
-                       histogram_dev, outD, outSize_dev, stream);
+                       histogram_dev, outD, outSize_dev, stream, &t);
 }
 
 static ANSDecodeStatus ansDecodeCommon(StackDeviceMemory& res, const ANSCodecConfig& config,
                                        uint32_t nb, const BatchDesc& in, const BatchDesc& out,
                                        uint32_t maxCap, uint8_t* succ, uint32_t* sizes,
-                                       hipStream_t s) {
+                                       hipStream_t s, const DeviceTables* tabs = nullptr) {
   ANSDecodeStatus status;
-  decodeBatchDevice<0>(res, config.probBits, nb, in, out, maxCap, succ, sizes, s);
+  decodeBatchDevice<0>(res, config.probBits, nb, in, out, maxCap, succ, sizes, s, tabs);
   if (config.useChecksum) {
-    status.errorInfo = verifyChecksums(res, nb, in, false, out, maxCap, s);
+    status.errorInfo = verifyChecksums(res, nb, in, false, out, maxCap, s, tabs);
     if (!status.errorInfo.empty()) status.error = ANSDecodeError::ChecksumMismatch;
   }
   return status;
@@ -433,11 +498,11 @@ ANSDecodeStatus ansDecodeBatchPointer(StackDeviceMemory& res, const ANSCodecConf
     cap[i] = outCapacity[i];
     maxCap = std::max(maxCap, cap[i]);
   }
-  auto t = uploadTables(res, stream, numInBatch, ip, op, cap);
-  auto inD = BatchDesc::pointers(t.u64a, nullptr);
-  auto outD = BatchDesc::pointers(t.u64b, t.u32a);
+  auto t = uploadTables(res, stream, numInBatch, ip, op, cap, true);
+  auto inD = t.tag(BatchDesc::pointers(t.u64a, nullptr));
+  auto outD = t.tag(BatchDesc::pointers(t.u64b, t.u32a));
   return ansDecodeCommon(res, config, numInBatch, inD, outD, maxCap, outSuccess_dev, outSize_dev,
-                         stream);
+                         stream, &t);
 }
 
 ANSDecodeStatus ansDecodeBatchSplitSize(StackDeviceMemory& res, const ANSCodecConfig& config,
@@ -462,11 +527,11 @@ ANSDecodeStatus ansDecodeBatchSplitSize(StackDeviceMemory& res, const ANSCodecCo
     run += outSplitSizes[i];
     maxCap = std::max(maxCap, sz[i]);
   }
-  auto t = uploadTables(res, stream, numInBatch, ip, off, sz);
-  auto inD = BatchDesc::pointers(t.u64a, nullptr);
-  auto outD = BatchDesc::split(out_dev, t.u64b, t.u32a);
+  auto t = uploadTables(res, stream, numInBatch, ip, off, sz, true);
+  auto inD = t.tag(BatchDesc::pointers(t.u64a, nullptr));
+  auto outD = t.tag(BatchDesc::split(out_dev, t.u64b, t.u32a));
   return ansDecodeCommon(res, config, numInBatch, inD, outD, maxCap, outSuccess_dev, outSize_dev,
-                         stream);
+                         stream, &t);
 }
 
 void ansGetCompressedInfoDevice(StackDeviceMemory& res, const void** in_dev, uint32_t numInBatch,
@@ -507,21 +572,25 @@ static void checkFloatConfig(const FloatCodecConfig& c) {
 
 void floatCompressDescs(StackDeviceMemory& res, const FloatCompressConfig& config, uint32_t nb,
                         const BatchDesc& in, uint32_t maxSize, const BatchDesc& out,
-                        uint32_t* outSize_dev, hipStream_t s) {
+                        uint32_t* outSize_dev, hipStream_t s, const DeviceTables* tabs) {
   checkFloatConfig(config);
   const int pb = config.ansConfig.probBits;
   switch (config.floatType) {
     case FloatType::kFloat16:
-      encodeBatchDevice<1>(res, pb, config.useChecksum, nb, in, maxSize, nullptr, out, outSize_dev, s);
+      encodeBatchDevice<1>(res, pb, config.useChecksum, nb, in, maxSize, nullptr, out, outSize_dev, s,
+                             tabs);
       break;
     case FloatType::kBFloat16:
-      encodeBatchDevice<2>(res, pb, config.useChecksum, nb, in, maxSize, nullptr, out, outSize_dev, s);
+      encodeBatchDevice<2>(res, pb, config.useChecksum, nb, in, maxSize, nullptr, out, outSize_dev, s,
+                             tabs);
       break;
     case FloatType::kFloat32:
-      encodeBatchDevice<3>(res, pb, config.useChecksum, nb, in, maxSize, nullptr, out, outSize_dev, s);
+      encodeBatchDevice<3>(res, pb, config.useChecksum, nb, in, maxSize, nullptr, out, outSize_dev, s,
+                             tabs);
       break;
     default:
-      encodeBatchDevice<4>(res, pb, config.useChecksum, nb, in, maxSize, nullptr, out, outSize_dev, s);
+      encodeBatchDevice<4>(res, pb, config.useChecksum, nb, in, maxSize, nullptr, out, outSize_dev, s,
+                             tabs);
       break;
   }
 }
@@ -530,28 +599,28 @@ FloatDecompressStatus floatDecompressDescs(StackDeviceMemory& res,
                                            const FloatDecompressConfig& config, uint32_t nb,
                                            const BatchDesc& in, const BatchDesc& out,
                                            uint32_t maxCap, uint8_t* succ, uint32_t* sizes,
-                                           hipStream_t s) {
+                                           hipStream_t s, const DeviceTables* tabs) {
   checkFloatConfig(config);
   const int pb = config.ansConfig.probBits;
   switch (config.floatType) {
     case FloatType::kFloat16:
-      decodeBatchDevice<1>(res, pb, nb, in, out, maxCap, succ, sizes, s);
+      decodeBatchDevice<1>(res, pb, nb, in, out, maxCap, succ, sizes, s, tabs);
       break;
     case FloatType::kBFloat16:
-      decodeBatchDevice<2>(res, pb, nb, in, out, maxCap, succ, sizes, s);
+      decodeBatchDevice<2>(res, pb, nb, in, out, maxCap, succ, sizes, s, tabs);
       break;
     case FloatType::kFloat32:
-      decodeBatchDevice<3>(res, pb, nb, in, out, maxCap, succ, sizes, s);
+      decodeBatchDevice<3>(res, pb, nb, in, out, maxCap, succ, sizes, s, tabs);
       break;
     default:
-      decodeBatchDevice<4>(res, pb, nb, in, out, maxCap, succ, sizes, s);
+      decodeBatchDevice<4>(res, pb, nb, in, out, maxCap, succ, sizes, s, tabs);
       break;
   }
   FloatDecompressStatus status;
   if (config.useChecksum) {
     // checksums `capacity` bytes (float words treated as bytes), as the
     // reference does (float/GpuFloatDecompress.cuh:1077-1112)
-    status.errorInfo = verifyChecksums(res, nb, in, true, out, maxCap, s);
+    status.errorInfo = verifyChecksums(res, nb, in, true, out, maxCap, s, tabs);
     if (!status.errorInfo.empty()) status.error = FloatDecompressError::ChecksumMismatch;
   }
   return status;
@@ -574,9 +643,9 @@ void floatCompress(StackDeviceMemory& res, const FloatCompressConfig& config, ui
     sz[i] = inSize[i];
     maxSize = std::max(maxSize, inSize[i]);
   }
-  auto t = uploadTables(res, stream, numInBatch, ip, op, sz);
-  floatCompressDescs(res, config, numInBatch, BatchDesc::pointers(t.u64a, t.u32a), maxSize,
-                     BatchDesc::pointers(t.u64b, nullptr), outSize_dev, stream);
+  auto t = uploadTables(res, stream, numInBatch, ip, op, sz, true);
+  floatCompressDescs(res, config, numInBatch, t.tag(BatchDesc::pointers(t.u64a, t.u32a)), maxSize,
+                     t.tag(BatchDesc::pointers(t.u64b, nullptr)), outSize_dev, stream, &t);
 }
 
 void floatCompressSplitSize(StackDeviceMemory& res, const FloatCompressConfig& config,
@@ -599,9 +668,9 @@ void floatCompressSplitSize(StackDeviceMemory& res, const FloatCompressConfig& c
     run += inSplitSizes[i];
     maxSize = std::max(maxSize, sz[i]);
   }
-  auto t = uploadTables(res, stream, numInBatch, off, {}, sz);
-  floatCompressDescs(res, config, numInBatch, BatchDesc::split(in_dev, t.u64a, t.u32a), maxSize,
-                     BatchDesc::strided(out_dev, outStride, 0), outSize_dev, stream);
+  auto t = uploadTables(res, stream, numInBatch, off, {}, sz, true);
+  floatCompressDescs(res, config, numInBatch, t.tag(BatchDesc::split(in_dev, t.u64a, t.u32a)),
+                     maxSize, BatchDesc::strided(out_dev, outStride, 0), outSize_dev, stream, &t);
 }
 
 void floatCompressBatchStride(StackDeviceMemory& res, const FloatCompressConfig& config,
@@ -635,10 +704,10 @@ FloatDecompressStatus floatDecompress(StackDeviceMemory& res, const FloatDecompr
     cap[i] = outCapacity[i];
     maxCap = std::max(maxCap, cap[i]);
   }
-  auto t = uploadTables(res, stream, numInBatch, ip, op, cap);
-  return floatDecompressDescs(res, config, numInBatch, BatchDesc::pointers(t.u64a, nullptr),
-                              BatchDesc::pointers(t.u64b, t.u32a), maxCap, outSuccess_dev,
-                              outSize_dev, stream);
+  auto t = uploadTables(res, stream, numInBatch, ip, op, cap, true);
+  return floatDecompressDescs(res, config, numInBatch, t.tag(BatchDesc::pointers(t.u64a, nullptr)),
+                              t.tag(BatchDesc::pointers(t.u64b, t.u32a)), maxCap, outSuccess_dev,
+                              outSize_dev, stream, &t);
 }
 
 FloatDecompressStatus floatDecompressSplitSize(StackDeviceMemory& res,
@@ -662,10 +731,10 @@ FloatDecompressStatus floatDecompressSplitSize(StackDeviceMemory& res,
     run += outSplitSizes[i];
     maxCap = std::max(maxCap, sz[i]);
   }
-  auto t = uploadTables(res, stream, numInBatch, ip, off, sz);
-  return floatDecompressDescs(res, config, numInBatch, BatchDesc::pointers(t.u64a, nullptr),
-                              BatchDesc::split(out_dev, t.u64b, t.u32a), maxCap, outSuccess_dev,
-                              outSize_dev, stream);
+  auto t = uploadTables(res, stream, numInBatch, ip, off, sz, true);
+  return floatDecompressDescs(res, config, numInBatch, t.tag(BatchDesc::pointers(t.u64a, nullptr)),
+                              t.tag(BatchDesc::split(out_dev, t.u64b, t.u32a)), maxCap,
+                              outSuccess_dev, outSize_dev, stream, &t);
 }
 
 FloatDecompressStatus floatDecompressBatchStride(StackDeviceMemory& res,

@@ -10,21 +10,24 @@
 
 namespace dietgpu {
 
+struct DeviceTables;  // codec.hip: per-call pointer tables (maybe kernel-argument inline)
+
 void floatCompressDescs(StackDeviceMemory& res, const FloatCompressConfig& config, uint32_t nb,
                         const BatchDesc& in, uint32_t maxSize, const BatchDesc& out,
-                        uint32_t* outSize_dev, hipStream_t s);
+                        uint32_t* outSize_dev, hipStream_t s, const DeviceTables* tabs = nullptr);
 
 FloatDecompressStatus floatDecompressDescs(StackDeviceMemory& res,
                                            const FloatDecompressConfig& config, uint32_t nb,
                                            const BatchDesc& in, const BatchDesc& out,
                                            uint32_t maxCap, uint8_t* succ, uint32_t* sizes,
-                                           hipStream_t s);
+                                           hipStream_t s, const DeviceTables* tabs = nullptr);
 
 // Compare archive checksums with the XOR of `decoded.size(b)` bytes of each
 // decoded element; synchronises `s`.
 std::vector<std::pair<int, std::string>> verifyChecksums(StackDeviceMemory& res, uint32_t nb,
                                                          const BatchDesc& archives, bool isFloat,
                                                          const BatchDesc& decoded,
-                                                         uint32_t maxBytes, hipStream_t s);
+                                                         uint32_t maxBytes, hipStream_t s,
+                                                         const DeviceTables* tabs = nullptr);
 
 }  // namespace dietgpu

@@ -80,10 +80,12 @@ __device__ __forceinline__ void stSc1(gp<uint32_t> p, uint32_t v) {
 
 // grid (nW, batch), 256 threads.  Workgroup x of element b owns blocks
 // [8x, 8x + 8); wave w codes blocks 8x + 2w (lanes 0-31) and 8x + 2w + 1
-// (lanes 32-63).
+// (lanes 32-63).  Pointer tables may ride in the first (InlineTable) argument (BatchDesc::field).  5 waves per SIMD (96 VGPRs, 32 of them the symbols; 27 KB
+// of LDS per workgroup).
 template <int FT, bool kCk>
-__global__ __launch_bounds__(cmp::kThreads) void k_compress(BatchDesc in, BatchDesc out,
-                                                            uint32_t batchOffset, CompScratch sc) {
+__global__ __launch_bounds__(cmp::kThreads) __attribute__((amdgpu_waves_per_eu(5, 8))) void k_compress(const InlineTable, BatchDesc in,
+                                                            BatchDesc out, uint32_t batchOffset,
+                                                            CompScratch sc) {
   using WordT = typename FloatTraits<FT>::WordT;
   static_assert(FloatTraits<FT>::kSegs == 1, "single-segment formats only");
   constexpr uint32_t kWPV = 16 / sizeof(WordT);                       // words per 16 B vector
@@ -138,9 +140,10 @@ __global__ __launch_bounds__(cmp::kThreads) void k_compress(BatchDesc in, BatchD
   const uint32_t nSeg = divUp(max(uwH[0], uwH[1]), cmp::kSegWords);
   gp<const WordT> blkSrc = src + uint64_t(blk) * kBlockSize;
 
-  // every segment's loads are issued D segments ahead (D = all 8 for up to 2
-  // vectors per lane, 3 for fp32): one HBM latency per workgroup, not eight
-  constexpr int D = V <= 2 ? int(cmp::kSegs) : 3;
+  // every segment's loads are issued D segments ahead (D = 4 for up to 2
+  // vectors per lane, 2 for fp32): about two HBM latencies per workgroup, not
+  // eight, within the 96 VGPRs of 5 waves per SIMD
+  constexpr int D = V <= 2 ? 4 : 2;
   auto phase1 = [&](auto vecTag) {
     constexpr bool kVec = decltype(vecTag)::value;
     uint4 pv[D][V];
@@ -183,6 +186,7 @@ __global__ __launch_bounds__(cmp::kThreads) void k_compress(BatchDesc in, BatchD
       // all of the segment's symbol reads first: an LDS read cannot be
       // hoisted over an earlier (possibly aliasing) ds_add, so interleaving
       // them would expose one LDS round trip per symbol
+      if (DG_EXP == 51) continue;  // counting experiment: no symbols / histogram
       const bool fullSeg = (g + 1) * cmp::kSegWords <= uw;
 #pragma unroll
       for (uint32_t t0 = 0; t0 < cmp::kSegSteps; t0 += 8) {
@@ -198,9 +202,13 @@ __global__ __launch_bounds__(cmp::kThreads) void k_compress(BatchDesc in, BatchD
                                  __HIP_MEMORY_SCOPE_WORKGROUP);
         }
 #pragma unroll
-        for (uint32_t r = 0; r < 2; ++r)
-          symR[g * 4 + t0 / 4 + r] =
-              sy[4 * r] | (sy[4 * r + 1] << 8) | (sy[4 * r + 2] << 16) | (sy[4 * r + 3] << 24);
+        for (uint32_t r = 0; r < 2; ++r) {
+          uint32_t packed = sy[4 * r] | (sy[4 * r + 1] << 8) | (sy[4 * r + 2] << 16) | (sy[4 * r + 3] << 24);
+          // opaque: otherwise the byte extractions of phase 2 fold back to
+          // the 128 unpacked symbol registers
+          asm volatile("" : "+v"(packed));
+          symR[g * 4 + t0 / 4 + r] = packed;
+        }
         __builtin_amdgcn_sched_barrier(0);
       }
       __builtin_amdgcn_wave_barrier();
@@ -314,7 +322,8 @@ __global__ __launch_bounds__(cmp::kThreads) void k_compress(BatchDesc in, BatchD
         __builtin_amdgcn_sched_barrier(0);
       }
     };
-    if (uwH[0] == kBlockSize && uwH[1] == kBlockSize)
+    if (DG_EXP == 50) {  // counting experiment: no encode
+    } else if (uwH[0] == kBlockSize && uwH[1] == kBlockSize)
       encode(std::true_type{});
     else
       encode(std::false_type{});

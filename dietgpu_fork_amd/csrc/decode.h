@@ -319,9 +319,11 @@ __device__ __forceinline__ void buildLut64(gp<const uint16_t> pdfIn, lp<u32x2> l
 
 // grid (ceil(maxBlocks / (kBlocksPerWG * chunksPerWG)), batch), dynamic LDS
 // DecCfg<FT>::ldsBytes(pb).  out.size(b) = capacity (bytes for raw ANS,
-// words for floats).
+// words for floats).  Pointer tables may ride in the first (InlineTable) argument
+// (BatchDesc::field).
 template <int FT, int KK>
-__global__ __launch_bounds__(dec::kThreads) void k_decode(BatchDesc in, BatchDesc out,
+__global__ __launch_bounds__(dec::kThreads) void k_decode(const InlineTable,
+                                                          BatchDesc in, BatchDesc out,
                                                           uint32_t batchOffset, int pb,
                                                           uint32_t chunksPerWG,
                                                           uint8_t* __restrict__ outSuccess,

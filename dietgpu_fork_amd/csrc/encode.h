@@ -242,11 +242,26 @@ __device__ __forceinline__ uint32_t normalizeCount(uint32_t count, uint32_t tota
 //   y = magic                         x / pdf == (umulhi(x, magic) + x) >> shift
 //   z = cdf
 //   w = (2^pb - pdf) | shift << 24    x' = x + cdf + (x / pdf) * (2^pb - pdf)
+// magic(q) = 2^32 * (2^shift - q) / q + 1 with shift = ceil(log2 q), for
+// every pdf 1 <= q <= 2^11, computed at compile time (a 64-bit division per
+// symbol is ~100 VALU instructions)
+struct MagicTable {
+  uint32_t m[(1u << 11) + 1];
+  constexpr MagicTable() : m() {
+    for (uint32_t q = 1; q <= (1u << 11); ++q) {
+      uint32_t sh = 0;
+      while ((1u << sh) < q) ++sh;
+      m[q] = uint32_t(((1ull << 32) * ((1ull << sh) - q)) / q + 1);
+    }
+  }
+};
+__device__ constexpr MagicTable kMagic{};
+
 __device__ __forceinline__ uint4 encTableEntry(uint32_t q, uint32_t cdf, int pb) {
   uint32_t shift = 0, magic = 0;
   if (q > 0) {
     shift = 32 - __clz(q - 1);
-    magic = uint32_t(((1ull << 32) * ((1ull << shift) - q)) / q + 1);
+    magic = kMagic.m[q];
   }
   return make_uint4(q << (kStateBits - pb), magic, cdf, ((1u << pb) - q) | (shift << 24));
 }
@@ -590,7 +605,7 @@ __device__ __forceinline__ uint32_t lookBack(gp<uint64_t> f, uint32_t x, uint32_
 // words 0-2 and 4-7, the pdf table, float header words 0-3 and 5-7, and the
 // raw section's rounding tails.  Whole workgroup.
 template <int FT>
-__device__ void writeHeadFixed(gp<uint8_t> base, gp<uint8_t> o, uint32_t n, uint32_t nBlocks,
+__device__ __forceinline__ void writeHeadFixed(gp<uint8_t> base, gp<uint8_t> o, uint32_t n, uint32_t nBlocks,
                                const EncTail& t, uint32_t b) {
   const uint32_t tid = threadIdx.x;
   const bool ansCk = FT == 0 && t.useChecksum;
@@ -631,7 +646,7 @@ __device__ void writeHeadFixed(gp<uint8_t> base, gp<uint8_t> o, uint32_t n, uint
 
 // The fields that need the element's word total (last workgroup, one lane).
 template <int FT>
-__device__ void writeHeadTotal(gp<uint8_t> base, gp<uint8_t> o, uint32_t n, uint32_t nBlocks,
+__device__ __forceinline__ void writeHeadTotal(gp<uint8_t> base, gp<uint8_t> o, uint32_t n, uint32_t nBlocks,
                                uint32_t totalWords, gp<uint2> bwords, const EncTail& t, uint32_t b) {
   ((gp<uint32_t>)o)[3] = totalWords;
   if (nBlocks & 1) st8(bwords + nBlocks, make_uint2(0, 0));

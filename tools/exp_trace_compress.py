@@ -36,6 +36,8 @@ stream = torch.cuda.current_stream(dev).cuda_stream
 for _ in range(3):
     N.check(L.dietgpu_float_compress(ws.h, ft, pb, 0, nb, in_ptrs, u, comp_ptrs, sizes.data_ptr(), stream))
 torch.cuda.synchronize()
+if not hasattr(L, "dietgpu_debug_read"):  # not a trace build (PMC runs)
+    sys.exit(0)
 buf = np.zeros(16384 * 24, dtype=np.uint64)
 L.dietgpu_debug_read.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
 assert L.dietgpu_debug_read(buf.ctypes.data, buf.nbytes) == 0
