@@ -156,22 +156,22 @@ bool compressSinglePass(StackDeviceMemory& res, int pb, bool useChecksum, uint32
 
   auto part = res.alloc<uint32_t>(s, size_t(nb) * nW * kNumSymbols);
   auto partCk = res.alloc<uint32_t>(s, kCk ? size_t(nb) * nW : 1);
-  // one zeroed region: look-back flags, then the per-element sync records
-  const size_t flagBytes = roundUp64(uint64_t(nb) * nW * 8, 256);
-  const size_t syncBytes = size_t(nb) * cmp::kSyncWords * 4;
-  auto zeroed = res.alloc<uint8_t>(s, flagBytes + syncBytes);
   auto slotMem = res.alloc<uint8_t>(s, size_t(nb) * std::max(MB, 1u) * kSlotDataBytes);
   auto ck = res.alloc<uint32_t>(s, FT != 0 && useChecksum ? nb : 1);
   DeviceDescs dd(res, s, FT != 0 && useChecksum ? tabs : nullptr);  // k_checksum's view
-  HIP_CHECK(hipMemsetAsync(zeroed.data(), 0, flagBytes + syncBytes, s));
+  // epoch-tagged flags in this stream's persistent arena: look-back flags,
+  // then team arrivals (no per-call zeroing)
+  const size_t flagBytes = roundUp64(uint64_t(nb) * nW * 8, 256);
+  SyncLease lease(s, flagBytes + size_t(nb) * nW * 4);
   if (FT != 0 && useChecksum) {
     HIP_CHECK(hipMemsetAsync(ck.data(), 0, sizeof(uint32_t) * nb, s));
   }
   CompScratch sc;
   sc.part = part.data();
   sc.partCk = partCk.data();
-  sc.flags = reinterpret_cast<uint64_t*>(zeroed.data());
-  sc.sync = reinterpret_cast<uint32_t*>(zeroed.data() + flagBytes);
+  sc.flags = reinterpret_cast<uint64_t*>(lease.base);
+  sc.arrive = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(lease.base) + flagBytes);
+  sc.epoch = lease.epoch;
   sc.slots = slotMem.data();
   sc.ckIn = FT != 0 && useChecksum ? ck.data() : nullptr;
   sc.outSize = outSize_dev;

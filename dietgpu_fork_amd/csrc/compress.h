@@ -36,6 +36,7 @@
 #pragma once
 
 #include "encode.h"
+#include "sync_arena.h"
 
 namespace dietgpu {
 
@@ -49,7 +50,6 @@ constexpr uint32_t kSegWords = kSegSteps * kLanesPerBlock;  // 512 symbols
 constexpr uint32_t kSegs = kSteps / kSegSteps;               // 8
 constexpr uint32_t kRing = 1024;  // u16 words per block ring (a typical block's whole output)
 constexpr uint32_t kSpill = 768;  // pending words that trigger a 256-word spill to the slot
-constexpr uint32_t kSyncWords = 32;   // per element: [0] arrivals (own 128 B line)
 constexpr uint32_t kSpinCap = 1u << 24;
 // Largest team (workgroups per element, i.e. up to 1 MiB of symbols): larger
 // teams wait longer at the barrier than a second read of the input costs, so
@@ -60,14 +60,15 @@ constexpr uint32_t kMaxTeam = 32;
 struct CompScratch {
   uint32_t* part;     // [nb][nW][256] partial histograms (sc1)
   uint32_t* partCk;   // [nb][nW] partial byte checksums (FT 0 with checksum)
-  uint32_t* sync;     // [nb][kSyncWords], zeroed before the launch
-  uint64_t* flags;    // [nb][nW] look-back flags, zeroed before the launch
+  uint32_t* arrive;   // [nb][nW] team arrival flags = epoch (sync arena)
+  uint64_t* flags;    // [nb][nW] look-back flags {status:2, epoch:30, value:32} (sync arena)
   uint8_t* slots;     // [nb][MB][kSlotDataBytes] spill space for dense blocks
   const uint32_t* ckIn;  // float checksum per element (k_checksum) or null
   uint32_t* outSize;
   uint32_t nW;        // workgroups per element row of the grid
   uint32_t MB;        // max blocks per element
   int pb;
+  uint32_t epoch;     // this call's epoch (SyncLease)
   bool useChecksum;
 };
 
@@ -76,6 +77,46 @@ __device__ __forceinline__ uint32_t ldSc1(gp<const uint32_t> p) {
 }
 __device__ __forceinline__ void stSc1(gp<uint32_t> p, uint32_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Decoupled look-back over the element's earlier workgroups (lookBack in
+// encode.h) with epoch-tagged flags: bits 63:62 status (1 aggregate, 2
+// inclusive prefix), 61:32 epoch, 31:0 value; a flag of another epoch reads
+// as "not yet published".  Called by one whole wave; returns the sum of the
+// values of workgroups [0, x).
+__device__ __forceinline__ uint32_t lookBackEpoch(gp<uint64_t> f, uint32_t x, uint32_t agg,
+                                                  uint32_t epoch) {
+  const uint32_t lane = laneId();
+  const uint64_t tag = uint64_t(epoch) << 32;
+  if (lane == 0)
+    __hip_atomic_store(f + x, (x == 0 ? kFlagPrefix : kFlagAgg) | tag | agg, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  if (x == 0) return 0;
+  uint32_t excl = 0;
+  int32_t j = int32_t(x);
+  for (uint32_t spins = 0; spins < cmp::kSpinCap;) {
+    const int32_t k = j - 1 - int32_t(lane);
+    const uint64_t v = k >= 0 ? __hip_atomic_load(f + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                              : (kFlagPrefix | tag);
+    const uint32_t hi = uint32_t(v >> 32);
+    const uint32_t status = (hi & kEpochMask) == epoch ? hi >> 30 : 0u;
+    const uint64_t isPre = ballot(status == 2);
+    const uint64_t isZero = ballot(status == 0);
+    const uint32_t firstPre = isPre ? uint32_t(__builtin_ctzll(isPre)) : 64u;
+    const uint64_t need = firstPre >= 63 ? ~0ull : (2ull << firstPre) - 1;
+    if (isZero & need) {
+      __builtin_amdgcn_s_sleep(2);
+      ++spins;
+      continue;
+    }
+    excl += waveSum(lane <= firstPre ? uint32_t(v) : 0u);
+    if (firstPre < 64) break;
+    j -= 64;
+  }
+  if (lane == 0)
+    __hip_atomic_store(f + x, kFlagPrefix | tag | uint64_t(excl + agg), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  return excl;
 }
 
 // grid (nW, batch), 256 threads.  Workgroup x of element b owns blocks
@@ -101,7 +142,6 @@ __global__ __launch_bounds__(cmp::kThreads) __attribute__((amdgpu_waves_per_eu(5
   __shared__ uint32_t keys[kNumSymbols];
   __shared__ uint32_t red[cmp::kWaves];
   __shared__ uint32_t cwE[cmp::kBlocksPerWG], flE[cmp::kBlocksPerWG], preE[cmp::kBlocksPerWG];
-  __shared__ uint32_t bcast[2];
 
   const uint32_t b = batchOffset + blockIdx.y;
   const uint32_t x = blockIdx.x;
@@ -238,16 +278,19 @@ __global__ __launch_bounds__(cmp::kThreads) __attribute__((amdgpu_waves_per_eu(5
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  gp<uint32_t> sync = G(sc.sync) + uint64_t(b) * cmp::kSyncWords;
-  if (tid == 0)
-    bcast[0] = __hip_atomic_fetch_add(sync, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __syncthreads();
+  // Arrival: one sc1 flag store (= this call's epoch) after every wave's
+  // partial-histogram stores have completed.  Wave 0 then polls the team's
+  // flags (lane j: member j); every workgroup sums the team's partials itself
+  // (one hop; the host keeps teams small, kMaxTeam).
+  gp<uint32_t> arrive = G(sc.arrive) + uint64_t(b) * sc.nW;
+  if (tid == 0) stSc1(arrive + x, sc.epoch);
   DG_STAMP_RT(2);
-  // Every workgroup waits for all arrivals and sums the team's partials
-  // itself: one hop, and the host keeps teams small (kMaxTeam).
-  if (tid == 0 && bcast[0] != team - 1) {
-    for (uint32_t spins = 0; spins < cmp::kSpinCap && ldSc1(sync) < team; ++spins)
+  if (w == 0) {
+    for (uint32_t spins = 0; spins < cmp::kSpinCap; ++spins) {
+      const bool in = lane >= team || ldSc1(arrive + lane) == sc.epoch;
+      if (ballot(!in) == 0) break;
       __builtin_amdgcn_s_sleep(1);
+    }
   }
   __syncthreads();
   uint32_t q, ckE = 0;
@@ -346,7 +389,7 @@ __global__ __launch_bounds__(cmp::kThreads) __attribute__((amdgpu_waves_per_eu(5
     const uint32_t r = lane < nk ? roundUp(cwE[lane], 8) : 0u;
     const uint32_t inc = waveInclusiveScan(r);
     const uint32_t agg = readfirst(__shfl(inc, 63));
-    const uint32_t excl = lookBack(G(sc.flags) + uint64_t(b) * sc.nW, x, agg);
+    const uint32_t excl = lookBackEpoch(G(sc.flags) + uint64_t(b) * sc.nW, x, agg, sc.epoch);
     if (lane < nk) preE[lane] = excl + inc - r;
     if (lane == 0 && x == team - 1) {
       const EncTail t{nullptr, nullptr, sc.outSize, nullptr, 0, sc.pb, sc.useChecksum};
