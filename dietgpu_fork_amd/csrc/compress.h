@@ -173,6 +173,10 @@ __global__ __launch_bounds__(cmp::kThreads) __attribute__((amdgpu_waves_per_eu(5
   const bool vecIn = (reinterpret_cast<uintptr_t>(src) & 15) == 0;
   lp<uint8_t> myT = (lp<uint8_t>)&symT[2 * w + h][0];
   lp<uint32_t> hcol = (lp<uint32_t>)&pool[l];
+  // quad byte transpose of the symbols (phase 1): lane l = 4 qm + qr
+  const uint32_t qr = l & 3, qm = l >> 2;
+  const uint32_t sel1 = (qr & 2) ? 0x03020706u : 0x05040100u;
+  const uint32_t sel2 = (qr & 1) ? 0x03070105u : 0x06020400u;
   uint32_t symR[kRegs];
 #pragma unroll
   for (int i = 0; i < kRegs; ++i) symR[i] = 0;
@@ -223,33 +227,34 @@ __global__ __launch_bounds__(cmp::kThreads) __attribute__((amdgpu_waves_per_eu(5
       DG_STAMP_RT(6 + g);
       if (g + D < nSeg) load(g + D);
       __builtin_amdgcn_wave_barrier();
-      // all of the segment's symbol reads first: an LDS read cannot be
-      // hoisted over an earlier (possibly aliasing) ds_add, so interleaving
-      // them would expose one LDS round trip per symbol
       if (DG_EXP == 51) continue;  // counting experiment: no symbols / histogram
+      // Transpose: lane l = 4m + r reads the dwords of rows 4q + r (q < 4),
+      // columns 4m..4m+3, and a 4 x 4 byte transpose inside its quad (two
+      // DPP exchanges + v_perm) leaves it column l, steps 4q..4q+3, packed
+      // as phase 2 wants: 4 ds_read_b32 instead of 16 ds_read_u8.
+      uint32_t W[4];
+#pragma unroll
+      for (uint32_t q = 0; q < 4; ++q)
+        W[q] = *(lp<const uint32_t>)(myT + (4 * q + qr) * 32 + 4 * qm);
+#pragma unroll
+      for (uint32_t q = 0; q < 4; ++q) {
+        uint32_t p2 = uint32_t(__builtin_amdgcn_update_dpp(0, int(W[q]), 0x4E, 0xF, 0xF, false));
+        W[q] = __builtin_amdgcn_perm(p2, W[q], sel1);  // 16-bit halves with lane r ^ 2
+        uint32_t p1 = uint32_t(__builtin_amdgcn_update_dpp(0, int(W[q]), 0xB1, 0xF, 0xF, false));
+        W[q] = __builtin_amdgcn_perm(p1, W[q], sel2);  // bytes with lane r ^ 1
+        // opaque: otherwise phase 2's byte extractions would be folded back
+        // into 128 unpacked symbol registers
+        asm volatile("" : "+v"(W[q]));
+        symR[g * 4 + q] = W[q];
+      }
       const bool fullSeg = (g + 1) * cmp::kSegWords <= uw;
 #pragma unroll
-      for (uint32_t t0 = 0; t0 < cmp::kSegSteps; t0 += 8) {
-        uint32_t sy[8];
-#pragma unroll
-        for (uint32_t t = 0; t < 8; ++t) sy[t] = myT[(t0 + t) * 32 + l];
-#pragma unroll
-        for (uint32_t t = 0; t < 8; ++t) {
-          const uint32_t sym = sy[t];
-          uint32_t add = 1u << ((sym & 1u) << 4);
-          if (!fullSeg) add = g * cmp::kSegWords + (t0 + t) * 32 + l < uw ? add : 0u;
-          __hip_atomic_fetch_add(hcol + (sym >> 1) * 32, add, __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
-#pragma unroll
-        for (uint32_t r = 0; r < 2; ++r) {
-          uint32_t packed = sy[4 * r] | (sy[4 * r + 1] << 8) | (sy[4 * r + 2] << 16) | (sy[4 * r + 3] << 24);
-          // opaque: otherwise the byte extractions of phase 2 fold back to
-          // the 128 unpacked symbol registers
-          asm volatile("" : "+v"(packed));
-          symR[g * 4 + t0 / 4 + r] = packed;
-        }
-        __builtin_amdgcn_sched_barrier(0);
+      for (uint32_t t = 0; t < cmp::kSegSteps; ++t) {
+        const uint32_t sym = (W[t / 4] >> (8 * (t & 3))) & 0xffu;
+        uint32_t add = 1u << ((sym & 1u) << 4);
+        if (!fullSeg) add = g * cmp::kSegWords + t * 32 + l < uw ? add : 0u;
+        __hip_atomic_fetch_add(hcol + (sym >> 1) * 32, add, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_WORKGROUP);
       }
       __builtin_amdgcn_wave_barrier();
     }
