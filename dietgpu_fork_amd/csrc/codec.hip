@@ -9,6 +9,7 @@
 //   compress:   k_hist -> k_normalize -> k_encode (+ k_coalesce for fp64)
 //   decompress: k_decode (table build + rANS decode + float join fused)
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <sstream>
@@ -45,6 +46,12 @@ uint32_t residentSlots(const void* kernel, int threads, uint32_t dynLds) {
   HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
   HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, kernel, threads, dynLds));
   return uint32_t(std::max(1, cus) * std::max(1, perCU));
+}
+
+// tuning knob from the environment (A/B experiments), else `def`
+uint32_t envU32(const char* name, uint32_t def) {
+  const char* e = std::getenv(name);
+  return e && *e ? uint32_t(std::strtoul(e, nullptr, 10)) : def;
 }
 
 void checkProbBits(int pb) {
@@ -179,6 +186,14 @@ bool compressSinglePass(StackDeviceMemory& res, int pb, bool useChecksum, uint32
   sc.MB = std::max(MB, 1u);
   sc.pb = pb;
   sc.useChecksum = useChecksum;
+  // Generation scheduling (CompScratch): both only matter when the grid is
+  // several generations of resident workgroups.
+  static const uint32_t prefetchOn = envU32("DIETGPU_COMPRESS_PREFETCH", 0);
+  static const uint32_t staggerTicks = envU32("DIETGPU_COMPRESS_STAGGER", 0);
+  const bool multiGen = uint64_t(nW) * std::min(nb, kMaxGridY) > 2ull * slots;
+  sc.prefetchDist = multiGen && prefetchOn ? slots : 0u;
+  sc.staggerTicks = multiGen ? staggerTicks : 0u;
+  sc.staggerRows = slots / nW;
   for (uint32_t y0 = 0; y0 < nb; y0 += kMaxGridY) {
     const uint32_t ny = std::min(kMaxGridY, nb - y0);
     if (FT != 0 && useChecksum) {

@@ -69,6 +69,14 @@ struct CompScratch {
   uint32_t MB;        // max blocks per element
   int pb;
   uint32_t epoch;     // this call's epoch (SyncLease)
+  // Cross-generation prefetch: while it encodes, a workgroup pulls the input
+  // of the workgroup `prefetchDist` linear ids ahead (the one that will take
+  // over a slot about when this one exits) into the caches.  0: off.
+  uint32_t prefetchDist;
+  // Staggered start: odd element rows below staggerRows (the first
+  // generation) wait staggerTicks (100 MHz) before phase 1.  0: off.
+  uint32_t staggerTicks;
+  uint32_t staggerRows;
   bool useChecksum;
 };
 
@@ -151,6 +159,10 @@ __global__ __launch_bounds__(cmp::kThreads) __attribute__((amdgpu_waves_per_eu(5
   const uint32_t team = max(1u, divUp(nBlocks, cmp::kBlocksPerWG));
   if (x >= team) return;
   const uint32_t first = x * cmp::kBlocksPerWG;
+  if (sc.staggerTicks && (blockIdx.y & 1u) && blockIdx.y < sc.staggerRows) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (__builtin_amdgcn_s_memrealtime() - t0 < sc.staggerTicks) __builtin_amdgcn_s_sleep(16);
+  }
 
   for (uint32_t i = tid; i < cmp::kBlocksPerWG * cmp::kRing / 8; i += cmp::kThreads)
     *(lp<u32x4>)&pool[4 * i] = u32x4{0, 0, 0, 0};
@@ -325,6 +337,26 @@ __global__ __launch_bounds__(cmp::kThreads) __attribute__((amdgpu_waves_per_eu(5
   }
   __syncthreads();  // table visible; the histogram is dead, `pool` becomes the rings
   DG_STAMP_RT(3);
+
+  // Prefetch for the next generation (CompScratch::prefetchDist): LDS-DMA
+  // loads of that workgroup's input into this wave's dead transpose buffer
+  // (never read; drained by the vmcnt(0) after phase 2), so its phase 1
+  // reads from the caches and HBM streams while this workgroup encodes.
+  if (sc.prefetchDist) {
+    const uint32_t lin = blockIdx.y * gridDim.x + x + sc.prefetchDist;
+    const uint32_t y2 = lin / gridDim.x, x2 = lin - (lin / gridDim.x) * gridDim.x;
+    if (y2 < gridDim.y) {
+      const uint32_t b2 = batchOffset + y2;
+      const uint32_t n2 = in.size(b2);
+      const uint32_t w0 = x2 * cmp::kBlocksPerWG * kBlockSize;
+      gp<const uint8_t> s2 = (gp<const uint8_t>)((gp<const WordT>)startOf(in, b2) + w0);
+      if (w0 < n2 && (reinterpret_cast<uintptr_t>(s2) & 15) == 0) {
+        const uint32_t bytes = min(n2 - w0, cmp::kBlocksPerWG * kBlockSize) * uint32_t(sizeof(WordT));
+        for (uint32_t off = 16 * tid; off + 16 <= bytes; off += 16 * cmp::kThreads)
+          __builtin_amdgcn_global_load_lds((gp<void>)(s2 + off), (lp<void>)&symT[2 * w][0], 16, 0, 0);
+      }
+    }
+  }
 
   // ---------------- phase 2: rANS encode from registers ---------------------
   gp<uint8_t> base = startOf(out, b);

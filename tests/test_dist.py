@@ -75,3 +75,72 @@ def test_two_rank_gloo_size_gather(tmp_path):
         assert (offs % 16 == 0).all()
     for i in range(NB):
         assert np.array_equal(np.load(tmp_path / f"arch{i}.npy"), ref[i])
+
+
+class _OracleCodec:
+    """CPU stand-in for dist.GpuFloatCodec in gloo tests (bf16): the oracle's
+    float codec, same archives as the GPU path."""
+
+    def compress(self, tensors):
+        from oracle import oracle as O
+
+        arch = [O.float_compress(t.view(torch.int16).numpy().view(np.uint16), 2, 10)
+                for t in tensors]
+        comp = torch.zeros(len(arch), max(a.size for a in arch), dtype=torch.uint8)
+        for i, a in enumerate(arch):
+            comp[i, : a.size] = torch.from_numpy(a)
+        return comp, torch.tensor([a.size for a in arch], dtype=torch.int32)
+
+    def decompress(self, archives, outs):
+        from oracle import oracle as O
+
+        for a, o in zip(archives, outs):
+            st, words = O.float_decompress(a.numpy(), 2, 10)
+            assert st == 0 and words.size == o.numel()
+            o.view(torch.int16).copy_(torch.from_numpy(words.view(np.int16)))
+
+
+def _bf16(n, seed):
+    g = torch.Generator().manual_seed(seed)
+    return (torch.randn(n, generator=g) * (1 + seed % 3)).to(torch.bfloat16)
+
+
+def _gather_inputs(rank):  # k = 3 tensors per rank, sizes differ between ranks
+    return [_bf16(n, 10 * rank + i) for i, n in enumerate((1000 + 333 * rank, 5000, 77 * (rank + 1)))]
+
+
+def _a2a_input(src, dst):
+    return _bf16(700 + 1111 * src + 37 * dst, 100 + 10 * src + dst)
+
+
+def _cc_worker(rank, world, port, outdir):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from dietgpu_fork_amd import dist as D
+
+        got = D.all_gather_compressed(_gather_inputs(rank), codec=_OracleCodec())
+        for j, t in enumerate(got):
+            np.save(os.path.join(outdir, f"ag{rank}_{j}.npy"), t.view(torch.int16).numpy())
+        got = D.all_to_all_compressed([_a2a_input(rank, d) for d in range(world)],
+                                      codec=_OracleCodec())
+        for s, t in enumerate(got):
+            np.save(os.path.join(outdir, f"a2a{rank}_{s}.npy"), t.view(torch.int16).numpy())
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_gloo_compressed_collectives(tmp_path):
+    """all_gather_compressed / all_to_all_compressed deliver every tensor bit
+    for bit (world 2, gloo, the oracle codec standing in for the GPU one)."""
+    world = 2
+    mp.spawn(_cc_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    want = [t for r in range(world) for t in _gather_inputs(r)]
+    for rank in range(world):
+        for j, t in enumerate(want):
+            got = np.load(tmp_path / f"ag{rank}_{j}.npy")
+            assert np.array_equal(got, t.view(torch.int16).numpy()), (rank, j)
+        for s in range(world):
+            got = np.load(tmp_path / f"a2a{rank}_{s}.npy")
+            assert np.array_equal(got, _a2a_input(s, rank).view(torch.int16).numpy()), (rank, s)
