@@ -131,8 +131,13 @@ __device__ __forceinline__ uint32_t lookBackEpoch(gp<uint64_t> f, uint32_t x, ui
 // [8x, 8x + 8); wave w codes blocks 8x + 2w (lanes 0-31) and 8x + 2w + 1
 // (lanes 32-63).  Pointer tables may ride in the first (InlineTable) argument (BatchDesc::field).  5 waves per SIMD (96 VGPRs, 32 of them the symbols; 27 KB
 // of LDS per workgroup).
+#if DG_EXP == 90 || DG_EXP == 91
+#define DG_CMP_WPE 4  // experiment: 4 waves / SIMD (c2: exactly 4 generations)
+#else
+#define DG_CMP_WPE 5
+#endif
 template <int FT, bool kCk>
-__global__ __launch_bounds__(cmp::kThreads) __attribute__((amdgpu_waves_per_eu(5, 8))) void k_compress(const InlineTable, BatchDesc in,
+__global__ __launch_bounds__(cmp::kThreads) __attribute__((amdgpu_waves_per_eu(DG_CMP_WPE, 8))) void k_compress(const InlineTable, BatchDesc in,
                                                             BatchDesc out, uint32_t batchOffset,
                                                             CompScratch sc) {
   using WordT = typename FloatTraits<FT>::WordT;
@@ -199,7 +204,7 @@ __global__ __launch_bounds__(cmp::kThreads) __attribute__((amdgpu_waves_per_eu(5
   // every segment's loads are issued D segments ahead (D = 4 for up to 2
   // vectors per lane, 2 for fp32): about two HBM latencies per workgroup, not
   // eight, within the 96 VGPRs of 5 waves per SIMD
-  constexpr int D = V <= 2 ? 4 : 2;
+  constexpr int D = DG_EXP == 90 ? (V <= 2 ? 8 : 4) : (V <= 2 ? 4 : 2);
   auto phase1 = [&](auto vecTag) {
     constexpr bool kVec = decltype(vecTag)::value;
     uint4 pv[D][V];
@@ -271,10 +276,12 @@ __global__ __launch_bounds__(cmp::kThreads) __attribute__((amdgpu_waves_per_eu(5
       __builtin_amdgcn_wave_barrier();
     }
   };
+  if (DG_EXP == 92) __builtin_amdgcn_s_setprio(1);
   if (vecIn)
     phase1(std::true_type{});
   else
     phase1(std::false_type{});
+  if (DG_EXP == 92) __builtin_amdgcn_s_setprio(0);
   DG_STAMP_RT(1);
   __syncthreads();
 
@@ -402,6 +409,7 @@ __global__ __launch_bounds__(cmp::kThreads) __attribute__((amdgpu_waves_per_eu(5
         __builtin_amdgcn_sched_barrier(0);
       }
     };
+    if (DG_EXP == 93) __builtin_amdgcn_s_setprio(1);
     if (DG_EXP == 50) {  // counting experiment: no encode
     } else if (uwH[0] == kBlockSize && uwH[1] == kBlockSize)
       encode(std::true_type{});
@@ -415,6 +423,7 @@ __global__ __launch_bounds__(cmp::kThreads) __attribute__((amdgpu_waves_per_eu(5
       }
     }
   }
+  if (DG_EXP == 93) __builtin_amdgcn_s_setprio(0);
   DG_STAMP_RT(4);
   // spilled words are read back by other waves of this workgroup
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
