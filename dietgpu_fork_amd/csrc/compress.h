@@ -264,15 +264,24 @@ __global__ __launch_bounds__(cmp::kThreads) __attribute__((amdgpu_waves_per_eu(D
         asm volatile("" : "+v"(W[q]));
         symR[g * 4 + q] = W[q];
       }
-      const bool fullSeg = (g + 1) * cmp::kSegWords <= uw;
+      // count: counter pair sym >> 1, +1 in the half sym & 1 (1 or 1 << 16 as
+      // bfe + mad_u24); segments full for both blocks of the wave skip the
+      // per-symbol bounds select (a wave-uniform branch)
+      auto count = [&](auto maskTag) {
+        constexpr bool kMasked = decltype(maskTag)::value;
 #pragma unroll
-      for (uint32_t t = 0; t < cmp::kSegSteps; ++t) {
-        const uint32_t sym = (W[t / 4] >> (8 * (t & 3))) & 0xffu;
-        uint32_t add = 1u << ((sym & 1u) << 4);
-        if (!fullSeg) add = g * cmp::kSegWords + t * 32 + l < uw ? add : 0u;
-        __hip_atomic_fetch_add(hcol + (sym >> 1) * 32, add, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_WORKGROUP);
-      }
+        for (uint32_t t = 0; t < cmp::kSegSteps; ++t) {
+          const uint32_t wq = W[t / 4], sh = 8 * (t & 3);
+          uint32_t add = __umul24(__builtin_amdgcn_ubfe(wq, sh, 1), 0xffffu) + 1u;
+          if (kMasked) add = g * cmp::kSegWords + t * 32 + l < uw ? add : 0u;
+          __hip_atomic_fetch_add(hcol + ((wq >> sh) & 0xfeu) * 16, add, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+      };
+      if ((g + 1) * cmp::kSegWords <= min(uwH[0], uwH[1]))
+        count(std::false_type{});
+      else
+        count(std::true_type{});
       __builtin_amdgcn_wave_barrier();
     }
   };

@@ -395,8 +395,24 @@ __device__ __forceinline__ void ringFlushAll(EStream& p, uint32_t lane) {
 template <bool kMask, uint32_t kRing = enc::kRing>
 __device__ __forceinline__ void encStep(EStream& p, bool valid, const u32x4& e, uint32_t hv,
                                         uint32_t trashAddr) {
-  const bool wr = kMask ? (valid && p.x >= e.x) : (p.x >= e.x);
-  const uint64_t vote = ballot(wr);
+  bool wr = true;
+  uint64_t vote;
+  uint32_t x;  // the state after renormalisation
+  if constexpr (kMask) {
+    wr = valid && p.x >= e.x;
+    vote = ballot(wr);
+    x = wr ? (p.x >> kEncodedBits) : p.x;
+  } else {
+    // compare into VCC so the select is one v_cndmask with SDWA WORD_1 (x >> 16)
+    static_assert(kEncodedBits == 16, "WORD_1 select");
+    asm("v_cmp_ge_u32_e32 vcc, %2, %3\n\t"
+        "v_cndmask_b32_sdwa %0, %2, %2, vcc dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD "
+        "src1_sel:WORD_1\n\t"
+        "s_mov_b64 %1, vcc"
+        : "=v"(x), "=s"(vote)
+        : "v"(p.x), "v"(e.x)
+        : "vcc");
+  }
   const int32_t cLo = __popc(uint32_t(vote));
   const int32_t cHi = __popc(uint32_t(vote >> 32));
   // write index = nout + (#writers of my half below me); v_mbcnt over 64
@@ -413,7 +429,7 @@ __device__ __forceinline__ void encStep(EStream& p, bool valid, const u32x4& e, 
   uint32_t dst;
   asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(dst) : "v"(trashAddr), "v"(ringAddr), "s"(vote));
   *(lp<uint16_t>)size_t(dst) = uint16_t(p.x);
-  const uint32_t x = wr ? (p.x >> kEncodedBits) : p.x;
+  (void)wr;
   uint32_t q = __umulhi(x, e.y);
   q = (q + x) >> (e.w >> 24);
   const uint32_t xn = __umul24(q, e.w) + x + e.z;  // u24 ignores the shift byte
