@@ -255,9 +255,10 @@ __global__ __launch_bounds__(cmp::kThreads) __attribute__((amdgpu_waves_per_eu(D
         W[q] = *(lp<const uint32_t>)(myT + (4 * q + qr) * 32 + 4 * qm);
 #pragma unroll
       for (uint32_t q = 0; q < 4; ++q) {
-        uint32_t p2 = uint32_t(__builtin_amdgcn_update_dpp(0, int(W[q]), 0x4E, 0xF, 0xF, false));
+        // (mov_dpp, not update_dpp: no zeroed `old` register per exchange)
+        uint32_t p2 = uint32_t(__builtin_amdgcn_mov_dpp(int(W[q]), 0x4E, 0xF, 0xF, true));
         W[q] = __builtin_amdgcn_perm(p2, W[q], sel1);  // 16-bit halves with lane r ^ 2
-        uint32_t p1 = uint32_t(__builtin_amdgcn_update_dpp(0, int(W[q]), 0xB1, 0xF, 0xF, false));
+        uint32_t p1 = uint32_t(__builtin_amdgcn_mov_dpp(int(W[q]), 0xB1, 0xF, 0xF, true));
         W[q] = __builtin_amdgcn_perm(p1, W[q], sel2);  // bytes with lane r ^ 1
         // opaque: otherwise phase 2's byte extractions would be folded back
         // into 128 unpacked symbol registers
