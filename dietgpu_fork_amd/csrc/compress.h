@@ -55,6 +55,12 @@ constexpr uint32_t kSpinCap = 1u << 24;
 // teams wait longer at the barrier than a second read of the input costs, so
 // the host sends them down the three-kernel path.
 constexpr uint32_t kMaxTeam = 32;
+// phase-1 histogram: u32 counters, 16 columns (lane & 15) per bin, bin rows
+// padded to 17 dwords so lanes l and l + 16 (one column) rarely share a bank
+constexpr uint32_t kHistCols = 16;
+constexpr uint32_t kHistStride = kHistCols + 1;
+constexpr uint32_t kHistWords = 256 * kHistStride;
+constexpr uint32_t kPoolWords = kHistWords > kBlocksPerWG * kRing / 2 ? kHistWords : kBlocksPerWG * kRing / 2;
 }  // namespace cmp
 
 struct CompScratch {
@@ -146,9 +152,9 @@ __global__ __launch_bounds__(cmp::kThreads) __attribute__((amdgpu_waves_per_eu(D
   constexpr int V = int(cmp::kSegWords * sizeof(WordT) / (32 * 16));  // vectors / lane / segment
   constexpr int kRegs = int(cmp::kSteps / 4);                         // symbol registers
 
-  // hist (phase 1: u16 counter pairs, bin-major, one column per lane of a
-  // 32-lane group) and the output rings (phase 2) share `pool`
-  __shared__ __attribute__((aligned(16))) uint32_t pool[cmp::kBlocksPerWG * cmp::kRing / 2];
+  // hist (phase 1: bin-major u32 counters, cmp::kHistCols columns) and the
+  // output rings (phase 2) share `pool`
+  __shared__ __attribute__((aligned(16))) uint32_t pool[cmp::kPoolWords];
   __shared__ __attribute__((aligned(16))) uint32_t tblS[kNumSymbols * 4];
   __shared__ __attribute__((aligned(16))) uint8_t symT[cmp::kBlocksPerWG][cmp::kSegWords];
   __shared__ uint32_t trashS[cmp::kWaves][64];
@@ -169,8 +175,9 @@ __global__ __launch_bounds__(cmp::kThreads) __attribute__((amdgpu_waves_per_eu(D
     while (__builtin_amdgcn_s_memrealtime() - t0 < sc.staggerTicks) __builtin_amdgcn_s_sleep(16);
   }
 
-  for (uint32_t i = tid; i < cmp::kBlocksPerWG * cmp::kRing / 8; i += cmp::kThreads)
+  for (uint32_t i = tid; i < cmp::kHistWords / 4; i += cmp::kThreads)
     *(lp<u32x4>)&pool[4 * i] = u32x4{0, 0, 0, 0};
+  static_assert(cmp::kHistWords % 4 == 0, "16 B zeroing");
   __syncthreads();
 
   const uint32_t w = readfirst(tid >> 6), lane = tid & 63, h = lane >> 5, l = lane & 31;
@@ -189,7 +196,7 @@ __global__ __launch_bounds__(cmp::kThreads) __attribute__((amdgpu_waves_per_eu(D
   gp<uint8_t> raw = FT == 0 ? gp<uint8_t>(nullptr) : startOf(out, b) + 32;
   const bool vecIn = (reinterpret_cast<uintptr_t>(src) & 15) == 0;
   lp<uint8_t> myT = (lp<uint8_t>)&symT[2 * w + h][0];
-  lp<uint32_t> hcol = (lp<uint32_t>)&pool[l];
+  lp<uint32_t> hcol = (lp<uint32_t>)&pool[l & (cmp::kHistCols - 1)];
   // quad byte transpose of the symbols (phase 1): lane l = 4 qm + qr
   const uint32_t qr = l & 3, qm = l >> 2;
   const uint32_t sel1 = (qr & 2) ? 0x03020706u : 0x05040100u;
@@ -265,17 +272,17 @@ __global__ __launch_bounds__(cmp::kThreads) __attribute__((amdgpu_waves_per_eu(D
         asm volatile("" : "+v"(W[q]));
         symR[g * 4 + q] = W[q];
       }
-      // count: counter pair sym >> 1, +1 in the half sym & 1 (1 or 1 << 16 as
-      // bfe + mad_u24); segments full for both blocks of the wave skip the
-      // per-symbol bounds select (a wave-uniform branch)
+      // count: +1 at row sym (bfe + mad_u24 address, constant increment);
+      // segments full for both blocks of the wave skip the per-symbol bounds
+      // select (a wave-uniform branch)
       auto count = [&](auto maskTag) {
         constexpr bool kMasked = decltype(maskTag)::value;
 #pragma unroll
         for (uint32_t t = 0; t < cmp::kSegSteps; ++t) {
-          const uint32_t wq = W[t / 4], sh = 8 * (t & 3);
-          uint32_t add = __umul24(__builtin_amdgcn_ubfe(wq, sh, 1), 0xffffu) + 1u;
-          if (kMasked) add = g * cmp::kSegWords + t * 32 + l < uw ? add : 0u;
-          __hip_atomic_fetch_add(hcol + ((wq >> sh) & 0xfeu) * 16, add, __ATOMIC_RELAXED,
+          const uint32_t sym = __builtin_amdgcn_ubfe(W[t / 4], 8 * (t & 3), 8);
+          uint32_t add = 1u;
+          if (kMasked) add = g * cmp::kSegWords + t * 32 + l < uw ? 1u : 0u;
+          __hip_atomic_fetch_add(hcol + __umul24(sym, cmp::kHistStride), add, __ATOMIC_RELAXED,
                                  __HIP_MEMORY_SCOPE_WORKGROUP);
         }
       };
@@ -295,12 +302,12 @@ __global__ __launch_bounds__(cmp::kThreads) __attribute__((amdgpu_waves_per_eu(D
   DG_STAMP_RT(1);
   __syncthreads();
 
-  // partial histogram of this workgroup: bin tid, sum of its 32 columns
+  // partial histogram of this workgroup: bin tid, sum of its columns (the
+  // padded rows make the 32 lanes' reads of one column conflict free)
   {
     uint32_t cnt = 0;
-    const uint32_t row = (tid >> 1) * 32, sh = (tid & 1) * 16;
 #pragma unroll
-    for (uint32_t k = 0; k < 32; ++k) cnt += (pool[row + ((k + tid) & 31)] >> sh) & 0xffffu;
+    for (uint32_t k = 0; k < cmp::kHistCols; ++k) cnt += pool[tid * cmp::kHistStride + k];
     stSc1(G(sc.part) + (uint64_t(b) * sc.nW + x) * kNumSymbols + tid, cnt);
     if constexpr (kCk) {
       ck = (ck ^ (ck >> 8) ^ (ck >> 16) ^ (ck >> 24)) & 0xffu;
