@@ -343,14 +343,18 @@ void decodeBatchDevice(StackDeviceMemory& res, int pb, uint32_t nb, const BatchD
       const uint32_t chunks = std::max(1u, divUp(maxBlocks, Cfg::kBlocksPerWG));
       const uint32_t slots =
           residentSlots(reinterpret_cast<const void*>(&k_decode<FT, KK>), dec::kThreads, lds);
-      const uint32_t P = std::max(1u, uint32_t((uint64_t(chunks) * ny + slots / 2) / slots));
+      const uint32_t gens = DG_EXP == 96 ? 2u : 1u;  // (96: experiment, two generations)
+      const uint32_t P = std::max(1u, uint32_t((uint64_t(chunks) * ny + gens * slots / 2) / (gens * slots)));
       dim3 g(divUp(chunks, P), ny);
       k_decode<FT, KK><<<g, dec::kThreads, lds, s>>>(kernargTable(tabs), in, out, y0, pb, P,
                                                      outSuccess_dev, outSize_dev);
       HIP_LAUNCH_CHECK();
     }
   };
-  launch(std::integral_constant<int, 0>{});
+  if constexpr (DG_EXP == 95 && FT == 2)  // experiment: two block pairs per wave
+    launch(std::integral_constant<int, 2>{});
+  else
+    launch(std::integral_constant<int, 0>{});
 }
 
 // Verify stored checksums against `unitBytes * out.size(b)` decoded bytes
