@@ -369,7 +369,18 @@ def _cpu_baseline(x, sample, pb, min_seconds=12.0, max_passes=40):
         te_s += te
         td_s += td
         passes += 1
+    # supplementary: the same oracle on 16 threads (the GPU box's CPU share;
+    # elements split across threads), a few seconds of work
+    T = min(16, os.cpu_count() or 1)
+    mt_tot = 0.0
+    mt_passes = 0
+    while mt_passes < max_passes and (mt_passes == 0 or mt_tot < 4.0):
+        mt_tot += O.time_float_roundtrip(words, 2, pb, threads=T)[0]
+        mt_passes += 1
+    multithread = {"value": round(mt_passes * U / mt_tot / 1e9, 4), "unit": "GB/s", "cores": T,
+                   "passes": mt_passes, "seconds": round(mt_tot, 3)}
     return {"value": round(passes * U / tot / 1e9, 4), "unit": "GB/s", "cores": 1, "kind": "port",
+            "multithread": multithread,
             "sample": f"{sample} x {words.shape[1] * 2 // 1048576} MiB bf16 of the c2 batch, "
                       f"{passes} passes of compress+decompress, serial C oracle "
                       f"(oracle/dietgpu_oracle.c), 1 thread",
