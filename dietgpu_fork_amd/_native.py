@@ -8,8 +8,7 @@ import os
 import subprocess
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-# DIETGPU_AMD_LIB: development override (kernel-variant experiments)
-LIB_PATH = os.environ.get("DIETGPU_AMD_LIB") or os.path.join(_HERE, "_lib", "libdietgpu_amd.so")
+LIB_PATH = os.path.join(_HERE, "_lib", "libdietgpu_amd.so")
 CSRC = os.path.join(_HERE, "csrc")
 
 DIETGPU_OK = 0

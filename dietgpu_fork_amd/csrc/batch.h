@@ -13,6 +13,9 @@
 
 namespace dietgpu {
 
+// constant address space (4): scalar (s_load) reads of read-only tables
+#define DG_CONST __attribute__((address_space(4)))
+
 // Per-call pointer / size / offset tables small enough to ride in the kernel
 // arguments of the hot kernels (k_compress, k_decode): the reference inlines
 // up to 128 pointers in its kernel parameters (BatchProviderInlinePointer,
@@ -47,8 +50,8 @@ struct BatchDesc {
   template <typename T>
   __device__ __forceinline__ T inlineAt(const void* field, uint32_t b) const {
 #if defined(__HIP_DEVICE_COMPILE__)  // (the host pass only parses device code)
-    const T* p = reinterpret_cast<const T*>((const uint8_t*)__builtin_amdgcn_kernarg_segment_ptr() +
-                                            reinterpret_cast<uintptr_t>(field));
+    const DG_CONST T* p = reinterpret_cast<const DG_CONST T*>(
+        (const DG_CONST uint8_t*)__builtin_amdgcn_kernarg_segment_ptr() + reinterpret_cast<uintptr_t>(field));
     const T v = p[b];
     if constexpr (sizeof(T) == 8) {
       const uint64_t u = uint64_t(v);
@@ -69,18 +72,31 @@ struct BatchDesc {
   __device__ __forceinline__ uint8_t* start(uint32_t b) const {
     if (mode == kPointer) {
       if (inl & kInlPtrs) return reinterpret_cast<uint8_t*>(inlineAt<uint64_t>(ptrs, b));
-      return reinterpret_cast<uint8_t*>(ptrs[b]);
+      return reinterpret_cast<uint8_t*>(tableAt(ptrs, b));
     }
     if (mode == kSplit) {
       if (inl & kInlOffsets) return base + inlineAt<uint64_t>(offsets, b);
-      return base + offsets[b];
+      return base + tableAt(offsets, b);
     }
     return base + stride * b;
   }
   __device__ __forceinline__ uint32_t size(uint32_t b) const {
     if (!sizes) return fixedSize;
     if (inl & kInlSizes) return inlineAt<uint32_t>(sizes, b);
-    return sizes[b];
+    return tableAt(sizes, b);
+  }
+
+  // Entry b of a device table (read-only for every kernel): through the
+  // constant address space, so a wave-uniform b becomes a scalar load that
+  // waits on lgkmcnt, not a vector load whose vmcnt(0) would also drain the
+  // kernel's streaming loads in flight.
+  template <typename T>
+  __device__ __forceinline__ static T tableAt(const T* table, uint32_t b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return ((const DG_CONST T*)table)[b];
+#else
+    return table[b];
+#endif
   }
 
   static BatchDesc strided(const void* p, uint64_t strideBytes, uint32_t size) {

@@ -11,17 +11,17 @@
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <memory>
+#include <mutex>
 #include <sstream>
+#include <tuple>
 #include <vector>
 
-#ifndef DG_EXP
-#define DG_EXP 0  // timing experiments only (make exp)
-#endif
 #include "codec_internal.h"
 #include "dietgpu/GpuANSCodec.h"
 #include "dietgpu/GpuFloatCodec.h"
-#include "compress.h"
+#include "pcompress.h"
 #include "decode.h"
 #include "encode.h"
 #include "profile.h"
@@ -33,25 +33,29 @@ constexpr uint32_t kMaxGridY = 65535;
 
 uint32_t histChunkWords(uint32_t nb, uint32_t maxSize) {
   uint32_t chunk = 64 * 1024;
-  const uint32_t target = DG_EXP == 30 ? 4096 : DG_EXP == 31 ? 8192 : DG_EXP == 32 ? 16384 : 2048;
+  const uint32_t target = 2048;
   while (chunk > 4096 && uint64_t(nb) * divUp(std::max(maxSize, 1u), chunk) < target) chunk /= 2;
   while (divUp(maxSize, chunk) > 4096) chunk *= 2;
   return chunk;
 }
 
-// workgroups of `kernel` resident on the whole device at once
+// workgroups of `kernel` resident on the whole device at once (cached per
+// device, kernel and LDS size: the queries cost host time on every call)
 uint32_t residentSlots(const void* kernel, int threads, uint32_t dynLds) {
-  int dev = 0, cus = 0, perCU = 0;
+  static std::mutex m;
+  static std::map<std::tuple<int, const void*, int, uint32_t>, uint32_t> cache;
+  int dev = 0;
   HIP_CHECK(hipGetDevice(&dev));
+  const auto key = std::make_tuple(dev, kernel, threads, dynLds);
+  std::lock_guard<std::mutex> g(m);
+  auto it = cache.find(key);
+  if (it != cache.end()) return it->second;
+  int cus = 0, perCU = 0;
   HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
   HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, kernel, threads, dynLds));
-  return uint32_t(std::max(1, cus) * std::max(1, perCU));
-}
-
-// tuning knob from the environment (A/B experiments), else `def`
-uint32_t envU32(const char* name, uint32_t def) {
-  const char* e = std::getenv(name);
-  return e && *e ? uint32_t(std::strtoul(e, nullptr, 10)) : def;
+  const uint32_t v = uint32_t(std::max(1, cus) * std::max(1, perCU));
+  cache[key] = v;
+  return v;
 }
 
 void checkProbBits(int pb) {
@@ -146,76 +150,112 @@ struct DeviceDescs {
 // ---------------------------------------------------------------------------
 // generic drivers
 // ---------------------------------------------------------------------------
-// Single-pass compression (k_compress, compress.h) for single-segment formats
-// without a caller-supplied histogram.  A team (the workgroups of one element)
-// meets at a barrier, so it must fit on the device with room to spare: at most
-// half the resident slots (each XCD then holds its ceil(team / 8) share).
+// Device error word: elements the compressor poisoned (a bounded wait ran out,
+// pcompress.h); its outSize is 0.  One per device (code object global).
+__device__ uint32_t g_dgErrors;
+
+uint32_t* deviceErrorWord() {
+  static std::mutex m;
+  static std::map<int, uint32_t*> addr;
+  int dev = 0;
+  HIP_CHECK(hipGetDevice(&dev));
+  std::lock_guard<std::mutex> g(m);
+  auto it = addr.find(dev);
+  if (it != addr.end()) return it->second;
+  void* p = nullptr;
+  HIP_CHECK(hipGetSymbolAddress(&p, HIP_SYMBOL(g_dgErrors)));
+  addr[dev] = static_cast<uint32_t*>(p);
+  return static_cast<uint32_t*>(p);
+}
+
+uint32_t deviceErrorCount(bool reset) {
+  uint32_t* p = deviceErrorWord();
+  HIP_CHECK(hipDeviceSynchronize());
+  uint32_t v = 0;
+  HIP_CHECK(hipMemcpy(&v, p, sizeof(v), hipMemcpyDeviceToHost));
+  if (reset && v) HIP_CHECK(hipMemset(p, 0, sizeof(v)));
+  return v;
+}
+
+// Single-pass compression (k_pcompress, pcompress.h) for single-segment
+// formats without a caller-supplied histogram, elements of at most
+// pc::kMaxTeam items (1 MiB of symbols).  One generation of resident
+// workgroups pulls items off the work queue.
 template <int FT, bool kCk>
-bool compressSinglePass(StackDeviceMemory& res, int pb, bool useChecksum, uint32_t nb,
+bool compressPersistent(StackDeviceMemory& res, int pb, bool useChecksum, uint32_t nb,
                         const BatchDesc& in, uint32_t maxSize, const BatchDesc& out,
                         uint32_t* outSize_dev, hipStream_t s, const DeviceTables* tabs) {
   const uint32_t MB = divUp(maxSize, kBlockSize);
-  const uint32_t nW = std::max(1u, divUp(MB, cmp::kBlocksPerWG));
-  static uint32_t slots = 0;
-  if (slots == 0)
-    slots = residentSlots(reinterpret_cast<const void*>(&k_compress<FT, kCk>), cmp::kThreads, 0);
-  if (DG_EXP == 40 || nW > cmp::kMaxTeam || uint64_t(nW) * 2 > slots) return false;
+  const uint32_t team = std::max(1u, divUp(MB, pc::kBlocksPerItem));
+  if (team > pc::kMaxTeam) return false;
+  const uint64_t items64 = uint64_t(team) * nb;
+  DG_CHECK(items64 < (1ull << 30), "batch too large for one compress call");
+  const uint32_t items = uint32_t(items64);
+  const uint32_t slots = residentSlots(reinterpret_cast<const void*>(&k_pcompress<FT, kCk>), pc::kThreads, 0);
+  // rounds of whole teams, balanced: R rounds of ceil(nb / R) teams
+  const uint32_t maxTeams = std::max(1u, slots / team);
+  const uint32_t rounds = divUp(nb, maxTeams);
+  uint32_t teamsPerRound = divUp(nb, rounds);
+  bool xcdTeams = false;
+  if (teamsPerRound >= 8 && roundUp(teamsPerRound, 8) <= maxTeams && divUp(nb, roundUp(teamsPerRound, 8)) == rounds) {
+    teamsPerRound = roundUp(teamsPerRound, 8);
+    xcdTeams = true;
+  }
+  const uint32_t grid = teamsPerRound * team;
 
-  auto part = res.alloc<uint32_t>(s, size_t(nb) * nW * kNumSymbols);
-  auto partCk = res.alloc<uint32_t>(s, kCk ? size_t(nb) * nW : 1);
-  auto slotMem = res.alloc<uint8_t>(s, size_t(nb) * std::max(MB, 1u) * kSlotDataBytes);
+  auto part = res.alloc<uint32_t>(s, size_t(items) * kNumSymbols);
+  auto partCk = res.alloc<uint32_t>(s, kCk ? items : 1);
+  auto slotMem = res.alloc<uint8_t>(s, size_t(grid) * pc::kBlocksPerItem * kSlotDataBytes);
   auto ck = res.alloc<uint32_t>(s, FT != 0 && useChecksum ? nb : 1);
   DeviceDescs dd(res, s, FT != 0 && useChecksum ? tabs : nullptr);  // k_checksum's view
   // epoch-tagged flags in this stream's persistent arena: look-back flags,
-  // then team arrivals (no per-call zeroing)
-  const size_t flagBytes = roundUp64(uint64_t(nb) * nW * 8, 256);
-  SyncLease lease(s, flagBytes + size_t(nb) * nW * 4);
+  // then team arrivals; the work-queue counter (no per-call zeroing)
+  const size_t flagBytes = roundUp64(uint64_t(items) * 8, 256);
+  SyncLease lease(res, s, flagBytes + size_t(items) * 4);
   if (FT != 0 && useChecksum) {
     HIP_CHECK(hipMemsetAsync(ck.data(), 0, sizeof(uint32_t) * nb, s));
-  }
-  CompScratch sc;
-  sc.part = part.data();
-  sc.partCk = partCk.data();
-  sc.flags = reinterpret_cast<uint64_t*>(lease.base);
-  sc.arrive = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(lease.base) + flagBytes);
-  sc.epoch = lease.epoch;
-  sc.slots = slotMem.data();
-  sc.ckIn = FT != 0 && useChecksum ? ck.data() : nullptr;
-  sc.outSize = outSize_dev;
-  sc.nW = nW;
-  sc.MB = std::max(MB, 1u);
-  sc.pb = pb;
-  sc.useChecksum = useChecksum;
-  // Generation scheduling (CompScratch): both only matter when the grid is
-  // several generations of resident workgroups.
-  static const uint32_t prefetchOn = envU32("DIETGPU_COMPRESS_PREFETCH", 0);
-  static const uint32_t staggerTicks = envU32("DIETGPU_COMPRESS_STAGGER", 0);
-  const bool multiGen = uint64_t(nW) * std::min(nb, kMaxGridY) > 2ull * slots;
-  sc.prefetchDist = multiGen && prefetchOn ? slots : 0u;
-  sc.staggerTicks = multiGen ? staggerTicks : 0u;
-  sc.staggerRows = slots / nW;
-  for (uint32_t y0 = 0; y0 < nb; y0 += kMaxGridY) {
-    const uint32_t ny = std::min(kMaxGridY, nb - y0);
-    if (FT != 0 && useChecksum) {
-      // float checksum: the reference passes float-word counts as byte counts
-      // (float/GpuFloatCompress.cuh:709)
-      const uint32_t ckChunk = 1u << 20;
+    // float checksum: the reference passes float-word counts as byte counts
+    // (float/GpuFloatCompress.cuh:709)
+    const uint32_t ckChunk = 1u << 20;
+    for (uint32_t y0 = 0; y0 < nb; y0 += kMaxGridY) {
+      const uint32_t ny = std::min(kMaxGridY, nb - y0);
       dim3 g(std::max(1u, divUp(maxSize, ckChunk)), ny);
       k_checksum<<<g, kThreads, 0, s>>>(dd.map(in), y0, 1, ckChunk, ck.data());
       HIP_LAUNCH_CHECK();
     }
-    prof::Scope p("compress", s);
-    k_compress<FT, kCk><<<dim3(nW, ny), cmp::kThreads, 0, s>>>(kernargTable(tabs), in, out, y0, sc);
-    HIP_LAUNCH_CHECK();
   }
+  PCompArgs a;
+  a.part = part.data();
+  a.partCk = partCk.data();
+  a.flags = reinterpret_cast<uint64_t*>(lease.base);
+  a.arrive = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(lease.base) + flagBytes);
+  a.err = deviceErrorWord();
+  a.slots = slotMem.data();
+  a.teamStart = nullptr;
+  a.ckIn = FT != 0 && useChecksum ? ck.data() : nullptr;
+  a.outSize = outSize_dev;
+  a.items = items;
+  a.team = team;
+  a.nb = nb;
+  a.grid = grid;
+  a.xcdTeams = xcdTeams ? 1u : 0u;
+  a.epoch = lease.epoch;
+  a.spinCap = spinCap();
+  a.pb = pb;
+  a.useChecksum = useChecksum;
+  prof::Scope p("compress", s);
+  k_pcompress<FT, kCk><<<grid, pc::kThreads, 0, s>>>(kernargTable(tabs), in, out, a);
+  HIP_LAUNCH_CHECK();
   return true;
 }
 
+// inAligned16: every element's input starts 16 B-aligned (the single-pass
+// compressor reads whole 16 B vectors; anything else takes three kernels)
 template <int FT>
 void encodeBatchDevice(StackDeviceMemory& res, int pb, bool useChecksum, uint32_t nb,
                        const BatchDesc& inArg, uint32_t maxSize, const uint32_t* hist_dev,
                        const BatchDesc& outArg, uint32_t* outSize_dev, hipStream_t s,
-                       const DeviceTables* tabs = nullptr) {
+                       const DeviceTables* tabs, bool inAligned16) {
   checkProbBits(pb);
   if (nb == 0) return;
   constexpr int kSegs = FloatTraits<FT>::kSegs;
@@ -227,10 +267,10 @@ void encodeBatchDevice(StackDeviceMemory& res, int pb, bool useChecksum, uint32_
   const bool runHist = !userHist || useChecksum;
   const bool rawCk = FT == 0 && useChecksum;
   if constexpr (kFused) {
-    if (!userHist) {
-      const bool done = rawCk ? compressSinglePass<FT, FT == 0>(res, pb, useChecksum, nb, inArg,
+    if (!userHist && inAligned16) {
+      const bool done = rawCk ? compressPersistent<FT, FT == 0>(res, pb, useChecksum, nb, inArg,
                                                                  maxSize, outArg, outSize_dev, s, tabs)
-                              : compressSinglePass<FT, false>(res, pb, useChecksum, nb, inArg, maxSize,
+                              : compressPersistent<FT, false>(res, pb, useChecksum, nb, inArg, maxSize,
                                                               outArg, outSize_dev, s, tabs);
       if (done) return;
     }
@@ -308,7 +348,8 @@ void encodeBatchDevice(StackDeviceMemory& res, int pb, bool useChecksum, uint32_
     if (MB > 0 || kFused) {
       prof::Scope p("encode", s);
       dim3 g(nW, ny);
-      const EncTail tail{pdf.data(), ck.data(), outSize_dev, flags.data(), nW, pb, useChecksum};
+      const EncTail tail{pdf.data(), ck.data(), outSize_dev, flags.data(), nW, pb, useChecksum,
+                         spinCap(), deviceErrorWord()};
       k_encode<FT, 0><<<g, enc::kThreads, 0, s>>>(in, out, y0, nb, std::max(MB, 1u), table.data(),
                                                slots.data(), cw.data(), tail);
       HIP_LAUNCH_CHECK();
@@ -343,18 +384,14 @@ void decodeBatchDevice(StackDeviceMemory& res, int pb, uint32_t nb, const BatchD
       const uint32_t chunks = std::max(1u, divUp(maxBlocks, Cfg::kBlocksPerWG));
       const uint32_t slots =
           residentSlots(reinterpret_cast<const void*>(&k_decode<FT, KK>), dec::kThreads, lds);
-      const uint32_t gens = DG_EXP == 96 ? 2u : 1u;  // (96: experiment, two generations)
-      const uint32_t P = std::max(1u, uint32_t((uint64_t(chunks) * ny + gens * slots / 2) / (gens * slots)));
+      const uint32_t P = std::max(1u, uint32_t((uint64_t(chunks) * ny + slots / 2) / slots));
       dim3 g(divUp(chunks, P), ny);
       k_decode<FT, KK><<<g, dec::kThreads, lds, s>>>(kernargTable(tabs), in, out, y0, pb, P,
                                                      outSuccess_dev, outSize_dev);
       HIP_LAUNCH_CHECK();
     }
   };
-  if constexpr (DG_EXP == 95 && FT == 2)  // experiment: two block pairs per wave
-    launch(std::integral_constant<int, 2>{});
-  else
-    launch(std::integral_constant<int, 0>{});
+  launch(std::integral_constant<int, 0>{});
 }
 
 // Verify stored checksums against `unitBytes * out.size(b)` decoded bytes
@@ -393,6 +430,12 @@ std::vector<std::pair<int, std::string>> verifyChecksums(StackDeviceMemory& res,
   return errs;
 }
 
+static bool allAligned16(const std::vector<uint64_t>& addrs) {
+  for (uint64_t a : addrs)
+    if (a % 16) return false;
+  return true;
+}
+
 static void checkOutAligned(const void* p, const char* what) {
   DG_CHECK(reinterpret_cast<uintptr_t>(p) % 16 == 0,
            what << " must be 16-byte aligned (archives are written with 16 B stores)");
@@ -420,8 +463,9 @@ void ansEncodeBatchStride(StackDeviceMemory& res, const ANSCodecConfig& config,
   DG_CHECK(outPerBatchStride % 16 == 0, "outPerBatchStride must be a multiple of 16");
   auto in = BatchDesc::strided(in_dev, inPerBatchStride, inPerBatchSize);
   auto out = BatchDesc::strided(out_dev, outPerBatchStride, 0);
+  const bool al = reinterpret_cast<uintptr_t>(in_dev) % 16 == 0 && inPerBatchStride % 16 == 0;
   encodeBatchDevice<0>(res, config.probBits, config.useChecksum, numInBatch, in, inPerBatchSize,
-                       histogram_dev, out, outBatchSize_dev, stream);
+                       histogram_dev, out, outBatchSize_dev, stream, nullptr, al);
 }
 
 void ansEncodeBatchPointer(StackDeviceMemory& res, const ANSCodecConfig& config,
@@ -443,7 +487,7 @@ void ansEncodeBatchPointer(StackDeviceMemory& res, const ANSCodecConfig& config,
   auto inD = t.tag(BatchDesc::pointers(t.u64a, t.u32a));
   auto outD = t.tag(BatchDesc::pointers(t.u64b, nullptr));
   encodeBatchDevice<0>(res, config.probBits, config.useChecksum, numInBatch, inD, maxSize,
-                       histogram_dev, outD, outSize_dev, stream, &t);
+                       histogram_dev, outD, outSize_dev, stream, &t, allAligned16(ip));
 }
 
 void ansEncodeBatchSplitSize(StackDeviceMemory& res, const ANSCodecConfig& config,
@@ -473,8 +517,9 @@ void ansEncodeBatchSplitSize(StackDeviceMemory& res, const ANSCodecConfig& confi
   auto t = uploadTables(res, stream, numInBatch, off, {}, sz, true);
   auto inD = t.tag(BatchDesc::split(in_dev, t.u64a, t.u32a));
   auto outD = BatchDesc::strided(out_dev, outStride, 0);
+  const bool al = reinterpret_cast<uintptr_t>(in_dev) % 16 == 0 && allAligned16(off);
   encodeBatchDevice<0>(res, config.probBits, config.useChecksum, numInBatch, inD, maxSize,
-                       histogram_dev, outD, outSize_dev, stream, &t);
+                       histogram_dev, outD, outSize_dev, stream, &t, al);
 }
 
 static ANSDecodeStatus ansDecodeCommon(StackDeviceMemory& res, const ANSCodecConfig& config,
@@ -591,25 +636,26 @@ static void checkFloatConfig(const FloatCodecConfig& c) {
 
 void floatCompressDescs(StackDeviceMemory& res, const FloatCompressConfig& config, uint32_t nb,
                         const BatchDesc& in, uint32_t maxSize, const BatchDesc& out,
-                        uint32_t* outSize_dev, hipStream_t s, const DeviceTables* tabs) {
+                        uint32_t* outSize_dev, hipStream_t s, const DeviceTables* tabs,
+                        bool inAligned16) {
   checkFloatConfig(config);
   const int pb = config.ansConfig.probBits;
   switch (config.floatType) {
     case FloatType::kFloat16:
       encodeBatchDevice<1>(res, pb, config.useChecksum, nb, in, maxSize, nullptr, out, outSize_dev, s,
-                             tabs);
+                             tabs, inAligned16);
       break;
     case FloatType::kBFloat16:
       encodeBatchDevice<2>(res, pb, config.useChecksum, nb, in, maxSize, nullptr, out, outSize_dev, s,
-                             tabs);
+                             tabs, inAligned16);
       break;
     case FloatType::kFloat32:
       encodeBatchDevice<3>(res, pb, config.useChecksum, nb, in, maxSize, nullptr, out, outSize_dev, s,
-                             tabs);
+                             tabs, inAligned16);
       break;
     default:
       encodeBatchDevice<4>(res, pb, config.useChecksum, nb, in, maxSize, nullptr, out, outSize_dev, s,
-                             tabs);
+                             tabs, inAligned16);
       break;
   }
 }
@@ -664,7 +710,8 @@ void floatCompress(StackDeviceMemory& res, const FloatCompressConfig& config, ui
   }
   auto t = uploadTables(res, stream, numInBatch, ip, op, sz, true);
   floatCompressDescs(res, config, numInBatch, t.tag(BatchDesc::pointers(t.u64a, t.u32a)), maxSize,
-                     t.tag(BatchDesc::pointers(t.u64b, nullptr)), outSize_dev, stream, &t);
+                     t.tag(BatchDesc::pointers(t.u64b, nullptr)), outSize_dev, stream, &t,
+                     allAligned16(ip));
 }
 
 void floatCompressSplitSize(StackDeviceMemory& res, const FloatCompressConfig& config,
@@ -689,7 +736,8 @@ void floatCompressSplitSize(StackDeviceMemory& res, const FloatCompressConfig& c
   }
   auto t = uploadTables(res, stream, numInBatch, off, {}, sz, true);
   floatCompressDescs(res, config, numInBatch, t.tag(BatchDesc::split(in_dev, t.u64a, t.u32a)),
-                     maxSize, BatchDesc::strided(out_dev, outStride, 0), outSize_dev, stream, &t);
+                     maxSize, BatchDesc::strided(out_dev, outStride, 0), outSize_dev, stream, &t,
+                     reinterpret_cast<uintptr_t>(in_dev) % 16 == 0 && allAligned16(off));
 }
 
 void floatCompressBatchStride(StackDeviceMemory& res, const FloatCompressConfig& config,
@@ -703,7 +751,8 @@ void floatCompressBatchStride(StackDeviceMemory& res, const FloatCompressConfig&
   floatCompressDescs(res, config, numInBatch,
                      BatchDesc::strided(in_dev, inPerBatchStrideBytes, inPerBatchWords),
                      inPerBatchWords, BatchDesc::strided(out_dev, outPerBatchStrideBytes, 0),
-                     outSize_dev, stream);
+                     outSize_dev, stream, nullptr,
+                     reinterpret_cast<uintptr_t>(in_dev) % 16 == 0 && inPerBatchStrideBytes % 16 == 0);
 }
 
 FloatDecompressStatus floatDecompress(StackDeviceMemory& res, const FloatDecompressConfig& config,
@@ -793,11 +842,3 @@ void floatGetCompressedInfo(StackDeviceMemory& res, const void** in, uint32_t nu
 }
 
 }  // namespace dietgpu
-
-#if DG_EXP == 7 || defined(DG_TRACE)
-extern "C" int dietgpu_debug_read(void* dst, size_t bytes) {
-  return hipMemcpyFromSymbol(dst, HIP_SYMBOL(dietgpu::g_dbgT), bytes, 0, hipMemcpyDeviceToHost) == hipSuccess
-             ? 0
-             : 2;
-}
-#endif

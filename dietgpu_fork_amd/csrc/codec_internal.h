@@ -14,7 +14,8 @@ struct DeviceTables;  // codec.hip: per-call pointer tables (maybe kernel-argume
 
 void floatCompressDescs(StackDeviceMemory& res, const FloatCompressConfig& config, uint32_t nb,
                         const BatchDesc& in, uint32_t maxSize, const BatchDesc& out,
-                        uint32_t* outSize_dev, hipStream_t s, const DeviceTables* tabs = nullptr);
+                        uint32_t* outSize_dev, hipStream_t s, const DeviceTables* tabs = nullptr,
+                        bool inAligned16 = false);
 
 FloatDecompressStatus floatDecompressDescs(StackDeviceMemory& res,
                                            const FloatDecompressConfig& config, uint32_t nb,

@@ -30,12 +30,7 @@
 
 #include "device.h"
 
-#ifndef DG_EXP
-#define DG_EXP 0  // timing experiments only (make exp): 0 = the real decoder
-#endif
-
 namespace dietgpu {
-// per-wave trace stamps (DG_STAMP / DG_STAMP_RT): device.h
 
 namespace dec {
 constexpr int kThreads = 256;
@@ -99,7 +94,6 @@ __device__ __forceinline__ void ringPrefetch(DStream& p, int hh, uint32_t lane, 
 // overwrites words >= lo + 256, all consumed since ptr < lo + 256) and
 // prefetch the next 256 words.
 __device__ __forceinline__ void ringEnsure(DStream& p, uint32_t lane, bool vec) {
-  if (DG_EXP == 3 || DG_EXP == 15) return;  // experiment: no refills
 #pragma unroll
   for (int hh = 0; hh < 2; ++hh) {
     if (p.lo[hh] > 0 && p.ptr[hh] - int32_t(32 * dec::kUnroll) < p.lo[hh]) {
@@ -378,7 +372,6 @@ __global__ __launch_bounds__(dec::kThreads) void k_decode(const InlineTable,
   const uint32_t w = readfirst(tid >> 6), lane = tid & 63, l = lane & 31;
   uint32_t hv = lane >= 32 ? ~0u : 0u;
   asm volatile("" : "+v"(hv));  // keep `hv & x` a v_and (not a v_cndmask pair)
-  DG_STAMP_RT(22);
 
   const bool vecIn = (reinterpret_cast<uintptr_t>(base) & 15) == 0;
   gp<uint8_t> outB = startOf(out, b);
@@ -492,7 +485,7 @@ __global__ __launch_bounds__(dec::kThreads) void k_decode(const InlineTable,
       auto join = [&](int32_t g, bool fullSeg, const uint32_t (&rv)[K][R]) {
         const uint32_t segW0 = uint32_t(g) * dec::kSegWords;
 #pragma unroll
-        for (int c = 0; c < K && DG_EXP != 1 && DG_EXP != 15; ++c) {
+        for (int c = 0; c < K; ++c) {
           const uint32_t uw = lane >= 32 ? uwH[c][1] : uwH[c][0];
           const uint32_t bk = blk0 + 2 * c + (lane >> 5);
           if (!fullSeg && segW0 + off >= uw) continue;
@@ -551,10 +544,8 @@ __global__ __launch_bounds__(dec::kThreads) void k_decode(const InlineTable,
         if (g > 0) loadRaw(g - 1, uint32_t(g - 1) < nFull, rvA);
       }
       // full segments: unrolled, unmasked
-      DG_STAMP(1);
       auto fullSeg = [&](int32_t g, const uint32_t (&cur)[K][R], uint32_t (&nxt)[K][R]) {
-        if (DG_EXP != 64)  // (64: without, for A/B runs)
-          setPrioRemaining((chunksPerWG - 1 - pass) * uint32_t(nSeg) + uint32_t(g), chunksPerWG * uint32_t(nSeg));
+        setPrioRemaining((chunksPerWG - 1 - pass) * uint32_t(nSeg) + uint32_t(g), chunksPerWG * uint32_t(nSeg));
         if (g > 0) loadRaw(g - 1, true, nxt);
 #pragma unroll
         for (int grp = int(dec::kSegSteps / dec::kUnroll) - 1; grp >= 0; --grp) {
@@ -574,7 +565,6 @@ __global__ __launch_bounds__(dec::kThreads) void k_decode(const InlineTable,
           }
         }
         __builtin_amdgcn_wave_barrier();
-        DG_STAMP(2 + (g & 15));
         join(g, true, cur);
         __builtin_amdgcn_wave_barrier();
       };
@@ -591,7 +581,6 @@ __global__ __launch_bounds__(dec::kThreads) void k_decode(const InlineTable,
       run(std::false_type{});
     __builtin_amdgcn_wave_barrier();
   }
-  DG_STAMP_RT(21);
 }
 
 }  // namespace dietgpu

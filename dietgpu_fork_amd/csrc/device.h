@@ -6,34 +6,6 @@
 
 namespace dietgpu {
 
-#ifndef DG_EXP
-#define DG_EXP 0  // timing experiments only (make exp)
-#endif
-#if DG_EXP == 7 || defined(DG_TRACE)
-// trace builds (make exp EXP=7, or EXPFLAGS=-DDG_TRACE): per-wave stamps
-// (lane 0), 24 slots per wave; read back with dietgpu_debug_read
-__device__ uint64_t g_dbgT[16384 * 24];
-#define DG_STAMP(slot)                                                                \
-  do {                                                                                \
-    if (lane == 0 && blockIdx.y * gridDim.x * 4 < 16384)                              \
-      g_dbgT[((blockIdx.y * gridDim.x + blockIdx.x) * 4 + w) * 24 + (slot)] =         \
-          __builtin_amdgcn_s_memtime();                                               \
-  } while (0)
-#define DG_STAMP_RT(slot)                                                             \
-  do {                                                                                \
-    if (lane == 0 && blockIdx.y * gridDim.x * 4 < 16384)                              \
-      g_dbgT[((blockIdx.y * gridDim.x + blockIdx.x) * 4 + w) * 24 + (slot)] =         \
-          __builtin_amdgcn_s_memrealtime();                                           \
-  } while (0)
-#else
-#define DG_STAMP(slot) \
-  do {                 \
-  } while (0)
-#define DG_STAMP_RT(slot) \
-  do {                    \
-  } while (0)
-#endif
-
 // Pointers into HBM carry address_space(1) so hipcc emits global_* (not
 // flat_*) memory instructions: flat ops count on both vmcnt and lgkmcnt and
 // force s_waitcnt vmcnt(0) lgkmcnt(0) at every LDS use.

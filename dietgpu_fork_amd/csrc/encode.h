@@ -59,19 +59,9 @@ __global__ __launch_bounds__(kThreads) void k_hist(BatchDesc in, uint32_t batchO
   uint32_t ck = 0;
   uint32_t* h0 = &hs[0][tid & (kHistCols - 1)];
   uint32_t* h1 = &hs[kSegs - 1][tid & (kHistCols - 1)];
-#ifndef DG_EXP
-#define DG_EXP 0
-#endif
-  uint32_t dummy = 0;
   auto addWord = [&](WordT w) {
-    if (DG_EXP == 8) {
-      h0[compOf<FT>(w, 0) * kHistCols] = tid;  // experiment: plain store
-    } else if (DG_EXP == 9) {
-      dummy += compOf<FT>(w, 0);  // experiment: no LDS
-    } else {
-      atomicAdd(&h0[compOf<FT>(w, 0) * kHistCols], 1u);
-      if constexpr (kSegs == 2) atomicAdd(&h1[compOf<FT>(w, 1) * kHistCols], 1u);
-    }
+    atomicAdd(&h0[compOf<FT>(w, 0) * kHistCols], 1u);
+    if constexpr (kSegs == 2) atomicAdd(&h1[compOf<FT>(w, 1) * kHistCols], 1u);
   };
 
   if (begin < size) {
@@ -133,7 +123,6 @@ __global__ __launch_bounds__(kThreads) void k_hist(BatchDesc in, uint32_t batchO
       if constexpr (kChecksum) ck ^= uint32_t(w);
     }
   }
-  if (DG_EXP == 9 && dummy == 0x12345678u) hs[0][0] = 1;
   __syncthreads();
   for (int s = 0; s < kSegs; ++s) {
     // bin tid: sum its 32 columns, rotated so the wave's reads spread banks
@@ -440,9 +429,11 @@ __device__ __forceinline__ void encStep(EStream& p, bool valid, const u32x4& e, 
 // -> the archive raw section at word index i0 (splitFloat's per-word split,
 // float/GpuFloatCompress.cuh:423-551; FloatTypeInfo::split,
 // float/GpuFloatUtils.cuh:190-370).
+// (store = false: symbols only, no raw-section store)
 template <int FT>
 __device__ __forceinline__ void splitVec(const uint4& v, uint32_t i0, uint32_t n,
-                                         gp<uint8_t> raw, lp<uint8_t> sym0, lp<uint8_t> sym1) {
+                                         gp<uint8_t> raw, lp<uint8_t> sym0, lp<uint8_t> sym1,
+                                         bool store = true) {
   using WordT = typename FloatTraits<FT>::WordT;
   const WordT* ws = reinterpret_cast<const WordT*>(&v);
   if constexpr (FT == 0) {
@@ -461,18 +452,20 @@ __device__ __forceinline__ void splitVec(const uint4& v, uint32_t i0, uint32_t n
     const uint32_t r0 = __builtin_amdgcn_perm(t[1], t[0], 0x06040200u);
     const uint32_t r1 = __builtin_amdgcn_perm(t[3], t[2], 0x06040200u);
     *(lp<u32x2>)sym0 = u32x2{e0, e1};
-    st8(raw + i0, make_uint2(r0, r1));
+    if (store) st8(raw + i0, make_uint2(r0, r1));
   } else if constexpr (FT == 3) {
     uint32_t r[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) r[k] = rotl32(ws[k], 1);
     *(lp<uint32_t>)sym0 = (__builtin_amdgcn_perm(r[1], r[0], 0x07030703u) & 0xffffu) |
                           (__builtin_amdgcn_perm(r[3], r[2], 0x07030703u) << 16);
-    st8(raw + 2 * i0, make_uint2(__builtin_amdgcn_perm(r[1], r[0], 0x05040100u),
-                                 __builtin_amdgcn_perm(r[3], r[2], 0x05040100u)));
-    *(gp<uint32_t>)(raw + 2 * roundUp(n, 8) + i0) =
-        (__builtin_amdgcn_perm(r[1], r[0], 0x06020602u) & 0xffffu) |
-        (__builtin_amdgcn_perm(r[3], r[2], 0x06020602u) << 16);
+    if (store) {
+      st8(raw + 2 * i0, make_uint2(__builtin_amdgcn_perm(r[1], r[0], 0x05040100u),
+                                   __builtin_amdgcn_perm(r[3], r[2], 0x05040100u)));
+      *(gp<uint32_t>)(raw + 2 * roundUp(n, 8) + i0) =
+          (__builtin_amdgcn_perm(r[1], r[0], 0x06020602u) & 0xffffu) |
+          (__builtin_amdgcn_perm(r[3], r[2], 0x06020602u) << 16);
+    }
   } else {
     const uint64_t r0 = rotl64(ws[0], 1), r1 = rotl64(ws[1], 1);
     *(lp<uint16_t>)sym0 = uint16_t((r0 >> 56) | ((r1 >> 56) << 8));
@@ -577,24 +570,33 @@ struct EncTail {
   uint32_t nW;
   int pb;
   bool useChecksum;
+  uint32_t spinCap = 1u << 24;  // look-back polls before the element is poisoned
+  uint32_t* err = nullptr;      // device error word (poisoned elements)
 };
 
 constexpr uint64_t kFlagAgg = 1ull << 62;
 constexpr uint64_t kFlagPrefix = 2ull << 62;
+constexpr uint64_t kFlagPoisonE = 1ull << 61;
 
 // Called by one whole wave; returns (wave-uniform) the sum of the values of
-// workgroups [0, x) of the element.
-__device__ __forceinline__ uint32_t lookBack(gp<uint64_t> f, uint32_t x, uint32_t agg) {
+// workgroups [0, x) of the element.  Predecessors were dispatched earlier, so
+// the wait is short; if it runs out of polls (`cap`) the flag chain is
+// POISONED instead (bit 61, carried forward by every later prefix) and
+// `poison` says whether any workgroup [0, x] of the element is poisoned: the
+// last one then writes outSize = 0 rather than a wrong archive.
+__device__ __forceinline__ uint32_t lookBack(gp<uint64_t> f, uint32_t x, uint32_t agg, uint32_t cap,
+                                             bool& poison) {
   const uint32_t lane = laneId();
+  poison = false;
   if (lane == 0)
     __hip_atomic_store((uint64_t*)f + x, (x == 0 ? kFlagPrefix : kFlagAgg) | agg, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
   if (x == 0) return 0;
   uint32_t excl = 0;
+  uint64_t pz = 0;
+  bool done = false;
   int32_t j = int32_t(x);
-  // predecessors are resident or done, so the wait is short; the cap only
-  // turns a logic error into a wrong archive instead of a hung device
-  for (uint32_t spins = 0; spins < (1u << 24);) {
+  for (uint32_t spins = 0; spins < cap;) {
     const int32_t k = j - 1 - int32_t(lane);
     const uint64_t v = k >= 0 ? __hip_atomic_load((uint64_t*)f + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                               : kFlagPrefix;
@@ -608,12 +610,18 @@ __device__ __forceinline__ uint32_t lookBack(gp<uint64_t> f, uint32_t x, uint32_
       continue;
     }
     excl += waveSum(lane <= firstPre ? uint32_t(v) : 0u);
-    if (firstPre < 64) break;
+    pz |= ballot(lane <= firstPre && (v & kFlagPoisonE) != 0);
+    if (firstPre < 64) {
+      done = true;
+      break;
+    }
     j -= 64;
   }
+  poison = pz != 0 || !done;
   if (lane == 0)
-    __hip_atomic_store((uint64_t*)f + x, kFlagPrefix | uint64_t(excl + agg), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store((uint64_t*)f + x,
+                       kFlagPrefix | (poison ? kFlagPoisonE : 0ull) | uint64_t(excl + agg),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   return excl;
 }
 
@@ -911,10 +919,17 @@ __global__ __launch_bounds__(enc::kThreads) void k_encode(BatchDesc in, BatchDes
       const uint32_t r = lane < nk ? roundUp(cwE[lane], 8) : 0u;
       const uint32_t inc = waveInclusiveScan(r);
       const uint32_t agg = readfirst(__shfl(inc, 63));
-      const uint32_t excl = DG_EXP == 21 ? 0u : lookBack(G(tail.flags) + uint64_t(b) * tail.nW, blockIdx.x, agg);
+      bool pz;
+      const uint32_t excl = lookBack(G(tail.flags) + uint64_t(b) * tail.nW, blockIdx.x, agg, tail.spinCap, pz);
       if (lane < nk) preE[lane] = excl + inc - r;
-      if (lane == 0 && (first + Cfg::kBlocksPerWG >= nBlocks))
-        writeHeadTotal<FT>(base, o, n, nBlocks, excl + agg, bwords, tail, b);
+      if (lane == 0 && (first + Cfg::kBlocksPerWG >= nBlocks)) {
+        if (pz) {
+          if (tail.outSize) G(tail.outSize)[b] = 0u;
+          __hip_atomic_fetch_add(G(tail.err), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+          writeHeadTotal<FT>(base, o, n, nBlocks, excl + agg, bwords, tail, b);
+        }
+      }
     }
     if (blockIdx.x == 0) writeHeadFixed<FT>(base, o, n, nBlocks, tail, b);
     __syncthreads();
@@ -923,7 +938,6 @@ __global__ __launch_bounds__(enc::kThreads) void k_encode(BatchDesc in, BatchDes
       const uint32_t uwk = min(kBlockSize, n - k * kBlockSize);
       st8(bwords + k, make_uint2((uwk << 16) | cwE[tid], preE[tid]));
     }
-    if (DG_EXP != 20)
     copyPayload(preE, cwE, nk, G(slots) + (uint64_t(b) * MB + first) * kSlotBytes + kStateBytesPerBlock,
                 (gp<uint8_t>)(bwords + roundUp(nBlocks, 2)));
   }

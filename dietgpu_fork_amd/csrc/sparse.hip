@@ -285,8 +285,9 @@ void sparseCompressT(StackDeviceMemory& res, const FloatCompressConfig& config, 
       HIP_LAUNCH_CHECK();
     }
   }
+  // (the compacted lists are 16 B-aligned slices of one arena allocation)
   floatCompressDescs(res, config, nb, BatchDesc::pointers(listPtrsDev.data(), listLen.data()),
-                     maxN, denseOut, outSize_dev, s);
+                     maxN, denseOut, outSize_dev, s, nullptr, true);
   if (outSize_dev) {
     k_sparseAddSizes<<<divUp(nb, 128), 128, 0, s>>>(in, nb, outSize_dev);
     HIP_LAUNCH_CHECK();

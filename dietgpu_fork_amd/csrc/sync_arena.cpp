@@ -1,15 +1,19 @@
 // Per-(device, stream) flag arenas for k_compress (see sync_arena.h).
 #include "sync_arena.h"
 
+#include <atomic>
+#include <functional>
 #include <map>
 #include <memory>
-#include <utility>
+#include <thread>
+#include <tuple>
 
 #include "common.h"
 
 namespace dietgpu {
 
 namespace {
+
 struct Arena {
   std::mutex m;
   void* ptr = nullptr;
@@ -17,20 +21,39 @@ struct Arena {
   uint32_t epoch = 0;
 };
 
+using Key = std::tuple<int, hipStream_t, size_t>;
 std::mutex gMapMutex;
-std::map<std::pair<int, hipStream_t>, std::unique_ptr<Arena>>& arenas() {
-  static auto* m = new std::map<std::pair<int, hipStream_t>, std::unique_ptr<Arena>>();
+std::map<Key, std::unique_ptr<Arena>>& arenas() {
+  static auto* m = new std::map<Key, std::unique_ptr<Arena>>();
   return *m;  // never destroyed: the runtime may be gone at exit
 }
+
+std::atomic<uint32_t> gSpinCap{1u << 24};
 }  // namespace
 
-SyncLease::SyncLease(hipStream_t stream, size_t bytes) {
+void setSpinCap(uint32_t polls) { gSpinCap.store(polls); }
+uint32_t spinCap() { return gSpinCap.load(); }
+
+SyncLease::SyncLease(StackDeviceMemory& res, hipStream_t stream, size_t bytes) {
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  HIP_CHECK(hipStreamIsCapturing(stream, &cs));
+  if (cs != hipStreamCaptureStatusNone) {
+    // graph capture: per-call state from the caller's arena, zeroed by a
+    // captured memset on every replay
+    capturing = true;
+    capMem_ = res.alloc<uint8_t>(stream, bytes);
+    HIP_CHECK(hipMemsetAsync(capMem_.data(), 0, bytes, stream));
+    base = capMem_.data();
+    epoch = 1;
+    return;
+  }
   int dev = 0;
   HIP_CHECK(hipGetDevice(&dev));
+  const size_t tkey = stream == hipStreamPerThread ? std::hash<std::thread::id>()(std::this_thread::get_id()) : 0;
   Arena* a;
   {
     std::lock_guard<std::mutex> g(gMapMutex);
-    auto& slot = arenas()[{dev, stream}];
+    auto& slot = arenas()[Key{dev, stream, tkey}];
     if (!slot) slot.reset(new Arena());
     a = slot.get();
   }
@@ -48,11 +71,11 @@ SyncLease::SyncLease(hipStream_t stream, size_t bytes) {
     zero = true;
   }
   a->epoch = (a->epoch + 1) & kEpochMask;
-  if (a->epoch == 0) {  // wrapped: flags of every older epoch must go
+  if (a->epoch == 0) zero = true;  // wrapped: flags of every older epoch must go
+  if (zero) {
+    HIP_CHECK(hipMemsetAsync(a->ptr, 0, a->bytes, stream));
     a->epoch = 1;
-    zero = true;
   }
-  if (zero) HIP_CHECK(hipMemsetAsync(a->ptr, 0, a->bytes, stream));
   base = a->ptr;
   epoch = a->epoch;
 }

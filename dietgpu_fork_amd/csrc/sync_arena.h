@@ -1,13 +1,21 @@
-// Persistent per-(device, stream) device memory for k_compress's
-// cross-workgroup flags (team arrivals, look-back prefixes).
+// Persistent per-(device, stream) device memory for the compressor's
+// cross-workgroup state: team-arrival flags and look-back flags of
+// k_pcompress.
 //
-// The flags carry a per-call epoch instead of being zeroed before every call:
-// a flag counts only if its epoch is the current call's, so stale values from
-// earlier calls are simply ignored and no memset launch precedes k_compress.
+// Flags carry a per-call epoch instead of being zeroed before every call: a
+// flag counts only if its epoch is the current call's, so stale values from
+// earlier calls are ignored and no memset launch precedes k_pcompress.
+//
 // Calls on one stream are serial, so one arena per (device, stream) keeps
-// concurrent calls on different streams apart; the lease holds the arena's
-// lock from epoch assignment to kernel launch, so host threads sharing a
-// stream enqueue epochs in order.
+// concurrent calls on different streams apart (hipStreamPerThread is keyed per
+// host thread, since that one handle names a different stream on each
+// thread); the lease holds the arena's lock from epoch assignment to kernel
+// launch, so host threads sharing a stream enqueue epochs in order.
+//
+// Under hipGraph stream capture every replay would reuse the captured epoch,
+// so a capturing call takes its flags from the caller's StackDeviceMemory
+// instead and zeroes them with a captured memset (a graph node that re-runs
+// on every replay); epoch 1.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -16,23 +24,38 @@
 #include <cstdint>
 #include <mutex>
 
+#include "dietgpu/StackDeviceMemory.h"
+
 namespace dietgpu {
 
-constexpr uint32_t kEpochMask = 0x3fffffffu;  // 30-bit epochs (flag bits 61:32)
+constexpr uint32_t kEpochMask = 0x1fffffffu;  // 29-bit epochs (flag bits 60:32)
 
 class SyncLease {
  public:
-  // A zero-initialised-at-creation region of >= bytes for the current device
-  // and `stream`, and this call's epoch (1 .. kEpochMask).
-  SyncLease(hipStream_t stream, size_t bytes);
+  // A region of >= `bytes` zero-at-creation bytes for the current device and
+  // `stream`, and this call's epoch (1 .. kEpochMask).
+  SyncLease(StackDeviceMemory& res, hipStream_t stream, size_t bytes);
   SyncLease(const SyncLease&) = delete;
   SyncLease& operator=(const SyncLease&) = delete;
 
   void* base = nullptr;
   uint32_t epoch = 0;
+  bool capturing = false;
 
  private:
+  GpuMemoryReservation<uint8_t> capMem_;
   std::unique_lock<std::mutex> lock_;
 };
+
+// Number of elements whose archive the compressor refused to finish since
+// the last reset (a team barrier or look-back wait ran out of polls: the
+// element's outSize is 0); synchronises the device.
+uint32_t deviceErrorCount(bool reset);
+
+// Polls allowed for each cross-workgroup wait of the compressor before it
+// gives up and poisons the element (default 1 << 24, about 0.5 s).  0 makes
+// every wait that has to wait fail: test hook for the error path.
+void setSpinCap(uint32_t polls);
+uint32_t spinCap();
 
 }  // namespace dietgpu
