@@ -36,6 +36,8 @@ def _declare(L):
     P = ctypes.c_void_p  # all device / host pointers passed as void*
     sig = {
         "dietgpu_last_error": (ctypes.c_char_p, []),
+        "dietgpu_device_error_count": (c_u32, [c_int]),
+        "dietgpu_set_spin_cap": (None, [c_u32]),
         "dietgpu_version": (ctypes.c_char_p, []),
         "dietgpu_stack_create": (vp, [c_int, P, c_size]),
         "dietgpu_stack_destroy": (None, [vp]),
@@ -111,6 +113,25 @@ def check(rc):
     if rc == DIETGPU_ERR_CHECKSUM:
         raise ChecksumMismatch(msg)
     raise DietGpuError(msg)
+
+
+def size_or_raise(v):
+    """A dietgpu_get_max_*compressed_size result: 0 means the C ABI caught an
+    error (e.g. an input too large for 32-bit archive sizes)."""
+    if v == 0:
+        raise DietGpuError(lib().dietgpu_last_error().decode(errors="replace") or
+                           "maximum compressed size query failed")
+    return v
+
+
+def check_archive_sizes(sizes):
+    """Compressed sizes read back to the host: 0 marks an element whose
+    compression was poisoned (a bounded cross-workgroup wait ran out; see
+    dietgpu_device_error_count in include/dietgpu_c.h)."""
+    bad = [i for i, v in enumerate(sizes) if int(v) == 0]
+    if bad:
+        raise DietGpuError(f"compression of batch element(s) {bad[:8]} was abandoned "
+                           f"(device error count {lib().dietgpu_device_error_count(1)})")
 
 
 def ptr_array(values):

@@ -35,15 +35,28 @@ def _ws(ws, device):
 
 
 def max_compressed_size(nbytes):
-    return N.lib().dietgpu_get_max_compressed_size(int(nbytes))
+    return N.size_or_raise(N.lib().dietgpu_get_max_compressed_size(int(nbytes)))
 
 
 def max_float_compressed_size(ft, words):
-    return N.lib().dietgpu_get_max_float_compressed_size(int(ft), int(words))
+    return N.size_or_raise(N.lib().dietgpu_get_max_float_compressed_size(int(ft), int(words)))
 
 
 def max_sparse_float_compressed_size(ft, words):
-    return N.lib().dietgpu_get_max_sparse_float_compressed_size(int(ft), int(words))
+    return N.size_or_raise(N.lib().dietgpu_get_max_sparse_float_compressed_size(int(ft),
+                                                                                 int(words)))
+
+
+def device_error_count(reset=True):
+    """Elements the compressor abandoned (outSize 0) since the last reset;
+    synchronises the device."""
+    return int(N.lib().dietgpu_device_error_count(int(reset)))
+
+
+def set_spin_cap(polls):
+    """Test hook: polls per cross-workgroup wait of the compressor (default
+    1 << 24; 0 makes every wait that has to wait fail)."""
+    N.lib().dietgpu_set_spin_cap(int(polls))
 
 
 # ------------------------------------------------------------------ ANS ----

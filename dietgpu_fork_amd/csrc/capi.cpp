@@ -11,6 +11,7 @@
 #include "dietgpu/GpuFloatCodec.h"
 #include "dietgpu/StackDeviceMemory.h"
 #include "profile.h"
+#include "sync_arena.h"
 
 using namespace dietgpu;
 
@@ -291,6 +292,17 @@ int dietgpu_float_decompress_batch_stride(dietgpu_stack* res, int ft, int pb, in
                                                  sizes, S(stream)));
   });
 }
+
+uint32_t dietgpu_device_error_count(int reset) {
+  uint32_t v = 0;
+  guarded([&] {
+    v = deviceErrorCount(reset != 0);
+    return DIETGPU_OK;
+  });
+  return v;
+}
+
+void dietgpu_set_spin_cap(uint32_t polls) { setSpinCap(polls); }
 
 void dietgpu_profile_enable(int on) { prof::setEnabled(on != 0); }
 void dietgpu_profile_filter(const char* kernel) { prof::setFilter(kernel); }

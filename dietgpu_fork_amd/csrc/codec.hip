@@ -625,6 +625,7 @@ uint32_t getMaxFloatCompressedSize(FloatType ft, uint32_t size) {
   DG_CHECK(ft != FloatType::kUndefined && uint32_t(ft) <= 4, "bad float type");
   uint64_t base = 32ull + getMaxCompressedSize(size) + floatRawBytes(int(ft), size);
   if (ft == FloatType::kFloat64) base += getMaxCompressedSize(size);
+  DG_CHECK(base <= uint64_t(INT32_MAX), "input too large: " << size << " float words");
   return uint32_t(base);
 }
 

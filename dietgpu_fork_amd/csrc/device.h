@@ -124,6 +124,29 @@ __device__ __forceinline__ uint32_t waveInclusiveScan(uint32_t v) {
   }
   return v;
 }
+// Wave64 sum / inclusive scan on the VALU (DPP within rows of 16 lanes, then
+// v_readlane across the four rows): no LDS-pipe shuffles (ds_bpermute),
+// whose round trips dominate short latency-bound sequences.
+__device__ __forceinline__ uint32_t waveSumDpp(uint32_t v) {
+  v += uint32_t(__builtin_amdgcn_mov_dpp(int(v), 0xB1, 0xF, 0xF, true));   // quad_perm [1,0,3,2]
+  v += uint32_t(__builtin_amdgcn_mov_dpp(int(v), 0x4E, 0xF, 0xF, true));   // quad_perm [2,3,0,1]
+  v += uint32_t(__builtin_amdgcn_mov_dpp(int(v), 0x141, 0xF, 0xF, true));  // row_half_mirror
+  v += uint32_t(__builtin_amdgcn_mov_dpp(int(v), 0x140, 0xF, 0xF, true));  // row_mirror
+  return uint32_t(__builtin_amdgcn_readlane(int(v), 0)) + uint32_t(__builtin_amdgcn_readlane(int(v), 16)) +
+         uint32_t(__builtin_amdgcn_readlane(int(v), 32)) + uint32_t(__builtin_amdgcn_readlane(int(v), 48));
+}
+__device__ __forceinline__ uint32_t waveInclusiveScanDpp(uint32_t v) {
+  v += uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x111, 0xF, 0xF, true));  // row_shr:1
+  v += uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x112, 0xF, 0xF, true));  // row_shr:2
+  v += uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x114, 0xF, 0xF, true));  // row_shr:4
+  v += uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x118, 0xF, 0xF, true));  // row_shr:8
+  const uint32_t r0 = uint32_t(__builtin_amdgcn_readlane(int(v), 15));
+  const uint32_t r1 = r0 + uint32_t(__builtin_amdgcn_readlane(int(v), 31));
+  const uint32_t r2 = r1 + uint32_t(__builtin_amdgcn_readlane(int(v), 47));
+  const uint32_t row = (threadIdx.x & 63) >> 4;
+  return v + (row == 0 ? 0u : row == 1 ? r0 : row == 2 ? r1 : r2);
+}
+
 template <int NT>
 __device__ __forceinline__ uint32_t blockSum(uint32_t v, uint32_t* smem) {
   constexpr int W = NT / 64;

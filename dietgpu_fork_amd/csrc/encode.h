@@ -255,6 +255,23 @@ __device__ __forceinline__ uint4 encTableEntry(uint32_t q, uint32_t cdf, int pb)
   return make_uint4(q << (kStateBits - pb), magic, cdf, ((1u << pb) - q) | (shift << 24));
 }
 
+// The same entry with the magic computed in registers (no dependent global
+// load of kMagic on a latency-bound path): floor((2^shift - q) 2^32 / q) + 1
+// from a double division (the numerator < 2^43 is exact; the quotient is
+// within one of the floor) and an exact integer fix-up.
+__device__ __forceinline__ uint4 encTableEntryReg(uint32_t q, uint32_t cdf, int pb) {
+  uint32_t shift = 0, magic = 0;
+  if (q > 0) {
+    shift = 32 - __clz(q - 1);
+    const uint64_t num = ((1ull << shift) - q) << 32;
+    uint64_t m = uint64_t(double(num) / double(q));
+    if (m * q > num) m -= 1;
+    else if ((m + 1) * q <= num) m += 1;
+    magic = uint32_t(m + 1);
+  }
+  return make_uint4(q << (kStateBits - pb), magic, cdf, ((1u << pb) - q) | (shift << 24));
+}
+
 // ---------------------------------------------------------------------------
 // k_normalize: one workgroup per (element, segment): sums the partial
 // histograms, normalises (normalizeCount) and stores the encode table rows

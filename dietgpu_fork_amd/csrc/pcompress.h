@@ -491,7 +491,7 @@ __global__ __launch_bounds__(pc::kThreads) __attribute__((amdgpu_waves_per_eu(4,
       ckOut = red[0] ^ red[1] ^ red[2] ^ red[3];
     }
     const uint32_t cdf = blockExclusiveScan<pc::kThreads>(q, red, nullptr);
-    const uint4 e = encTableEntry(q, cdf, A().pb);
+    const uint4 e = encTableEntryReg(q, cdf, A().pb);
     *(lp<u32x4>)&tblS[4 * tid] = u32x4{e.x, e.y, e.z, e.w};
     pdfS[tid] = uint16_t(q);
     __syncthreads();

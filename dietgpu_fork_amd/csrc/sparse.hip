@@ -356,7 +356,9 @@ FloatDecompressStatus sparseDecompressT(StackDeviceMemory& res,
 }  // namespace
 
 uint32_t getMaxSparseFloatCompressedSize(FloatType ft, uint32_t size) {
-  return 16 + roundUp((size + 7) / 8, 16) + getMaxFloatCompressedSize(ft, size);
+  const uint64_t v = 16ull + roundUp64((uint64_t(size) + 7) / 8, 16) + getMaxFloatCompressedSize(ft, size);
+  DG_CHECK(v <= uint64_t(INT32_MAX), "input too large: " << size << " float words");
+  return uint32_t(v);
 }
 
 void floatCompressSparse(StackDeviceMemory& res, const FloatCompressConfig& config,

@@ -70,24 +70,26 @@ def _stack_for(dev, temp_mem):
 def max_float_compressed_output_size(ts):
     """DietGpu.cpp:128-137 -> (rows, cols)"""
     _, mx = _total_and_max(ts)
-    cols = N.lib().dietgpu_get_max_float_compressed_size(_float_type(ts[0]), mx)
+    cols = N.size_or_raise(N.lib().dietgpu_get_max_float_compressed_size(_float_type(ts[0]), mx))
     return len(ts), cols
 
 
 def max_float_compressed_size(dtype, size):
     """DietGpu.cpp:140-142"""
-    return N.lib().dietgpu_get_max_float_compressed_size(_float_type(dtype), int(size))
+    return N.size_or_raise(N.lib().dietgpu_get_max_float_compressed_size(_float_type(dtype),
+                                                                         int(size)))
 
 
 def max_any_compressed_output_size(ts):
     """DietGpu.cpp:144-150"""
     _, mx = _total_and_max(ts)
-    return len(ts), N.lib().dietgpu_get_max_compressed_size(mx * ts[0].element_size())
+    return len(ts), N.size_or_raise(
+        N.lib().dietgpu_get_max_compressed_size(mx * ts[0].element_size()))
 
 
 def max_any_compressed_size(nbytes):
     """DietGpu.cpp:152-154"""
-    return N.lib().dietgpu_get_max_compressed_size(int(nbytes))
+    return N.size_or_raise(N.lib().dietgpu_get_max_compressed_size(int(nbytes)))
 
 
 # ------------------------------------------------------------- compress ----
@@ -157,6 +159,7 @@ def compress_data(compress_as_float, ts_in, checksum=False, temp_mem=None,
 def _matrix_to_tensors(n, matrix, sizes):
     """compressedMatrixToTensors, DietGpu.cpp:84-108"""
     host = sizes.to("cpu")
+    N.check_archive_sizes(host[:n].tolist())
     flat = matrix.view(-1)
     cols = matrix.size(1)
     return [flat.narrow(0, i * cols, int(host[i])) for i in range(n)]
@@ -183,8 +186,8 @@ def compress_data_split_size(compress_as_float, t_in, t_in_split_sizes, checksum
             _check(v % 4 == 0, "All splits should start on a 16 byte boundary; the size of an "
                    "interior split is not a multiple of 16 bytes")
     L = N.lib()
-    cols = (L.dietgpu_get_max_float_compressed_size(ft, mx) if compress_as_float
-            else L.dietgpu_get_max_compressed_size(mx))
+    cols = N.size_or_raise(L.dietgpu_get_max_float_compressed_size(ft, mx) if compress_as_float
+                           else L.dietgpu_get_max_compressed_size(mx))
     if out_compressed is not None:
         c = out_compressed
         _check(c.dtype == torch.uint8 and c.device.type == "cuda" and c.is_contiguous())
@@ -227,6 +230,7 @@ def compress_data_simple(compress_as_float, ts_in, checksum=False, temp_mem=6710
     comp, sizes, _ = compress_data(compress_as_float, ts_in, checksum, scratch)
     host = sizes.to("cpu")
     _check(host.size(0) == len(ts_in))
+    N.check_archive_sizes(host.tolist())
     cols = comp.size(1)
     flat = comp.view(-1)
     return [flat.narrow(0, i * cols, int(host[i])).clone() for i in range(len(ts_in))]

@@ -172,6 +172,20 @@ void dietgpu_profile_filter(const char* kernel);
 int dietgpu_profile_query(const char* kernel, double* total_ms, uint64_t* launches);
 void dietgpu_profile_reset(void);
 
+/* ---- compressor error reporting (MI355X extension) ----
+ * The single-pass compressor's cross-workgroup waits (team barrier, look-back)
+ * are bounded.  A wait that runs out POISONS its element instead of producing
+ * a wrong archive: that element's out_size is written as 0 (no valid archive
+ * is shorter than 544 bytes) and the device error word counts it.
+ * dietgpu_device_error_count synchronises the current device and returns the
+ * count since the last reset (reset != 0 clears it). */
+uint32_t dietgpu_device_error_count(int reset);
+/* Test hook: polls each such wait may make before it gives up (default
+ * 1 << 24).  0 makes every wait that would have to wait fail at once, which
+ * forces the error path deterministically for elements of more than one
+ * team member.  Passed to the kernels as an argument. */
+void dietgpu_set_spin_cap(uint32_t polls);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,65 @@
+"""Full-size GPU runs of the BASELINE.json configurations the bench quotes:
+c3 (1024 x 4 MiB bytes at 4 bit/symbol, ansEncodeBatchStride /
+ansDecodeBatchStride) and c5 at G=1 (8192 x 1 MiB bf16, the batch the
+multi-GPU bench shards).  Too large for a full oracle comparison in test
+time, so each checks the whole-batch roundtrip bit for bit on the device,
+the 16 B archive-size contract (GpuANSUtils.cuh:33 kBlockAlignment), and
+byte identity with the oracle for sampled elements (first, middle, last)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module")
+def C():
+    import dietgpu_fork_amd  # noqa: F401
+    from dietgpu_fork_amd import codec
+
+    return codec
+
+
+def test_c3_full(C):
+    nb, n = 1024, 4 << 20
+    g = torch.Generator(device=DEV).manual_seed(3)
+    x = torch.randint(0, 16, (nb, n), generator=g, device=DEV, dtype=torch.uint8)
+    ws = C.Workspace(1 << 30)
+    arch, sizes = C.ans_encode_stride(x, prob_bits=10, ws=ws)
+    s = sizes.cpu().numpy()
+    assert (s > 0).all() and (s % 16 == 0).all()
+    # 4 bit/symbol: about half the input (per-block states and headers aside)
+    assert 0.49 * n < s.mean() < 0.53 * n
+    out, ok, osz = C.ans_decode_stride(arch, n, prob_bits=10, ws=ws)
+    assert bool((ok == 1).all()) and bool((osz == n).all())
+    assert torch.equal(out, x)
+    del out
+    for i in (0, nb // 2 - 1, nb - 1):
+        ref = O.ans_encode(x[i].cpu().numpy(), 10, False)
+        assert s[i] == ref.size, i
+        np.testing.assert_array_equal(arch[i, : ref.size].cpu().numpy(), ref, err_msg=f"element {i}")
+
+
+def test_c5_single_gpu(C):
+    nb, n = 8192, 524288
+    x = torch.empty([nb, n], dtype=torch.bfloat16, device=DEV)
+    g = torch.Generator(device=DEV).manual_seed(5)
+    for r in range(0, nb, 512):
+        x[r:r + 512] = torch.randn([512, n], generator=g, device=DEV).to(torch.bfloat16)
+    ws = C.Workspace(1 << 30)
+    arch, sizes = C.float_compress_stride(x, prob_bits=10, ws=ws)
+    s = sizes.cpu().numpy()
+    assert (s > 0).all() and (s % 16 == 0).all()
+    assert C.device_error_count(reset=True) == 0
+    out, ok, osz = C.float_decompress_stride(arch, n, torch.bfloat16, prob_bits=10, ws=ws)
+    assert bool((ok == 1).all()) and bool((osz == n).all())
+    assert torch.equal(out.view(torch.int16), x.view(torch.int16))
+    del out
+    for i in (0, nb // 2 - 1, nb - 1):
+        ref = O.float_compress(x[i].view(torch.int16).cpu().numpy().view(np.uint16), 2)
+        assert s[i] == ref.size, i
+        np.testing.assert_array_equal(arch[i, : ref.size].cpu().numpy(), ref, err_msg=f"element {i}")

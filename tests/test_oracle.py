@@ -44,6 +44,23 @@ def test_kat_uniform():
     assert (pdf == 4).all()
 
 
+def test_kat_diff_positive_bumps_symbol_ids():
+    # SURVEY Appendix B.2, GpuANSStatistics.cuh:266-267: counts 3 at symbols
+    # 200..202 scale to 341 each (1023 < 1024); the diff>0 branch then adds
+    # the missing 1 to symbol id 0, which is absent from the input
+    h = np.zeros(256, dtype=np.uint32)
+    h[200:203] = 3
+    pdf, cdf = O.normalize(h, 9, 10)
+    assert pdf[200] == pdf[201] == pdf[202] == 341
+    assert pdf[0] == 1
+    assert int(pdf.sum()) == 1024 and int(np.count_nonzero(pdf)) == 4
+    assert cdf[200] == 1 and cdf[202] == 1 + 2 * 341
+    assert pdf.tolist() == pyref.normalize(h.tolist(), 9, 10)
+    d = np.repeat(np.arange(200, 203, dtype=np.uint8), 3)
+    st, dec = O.ans_decode(O.ans_encode(d, 10), 10)
+    assert st == 0 and np.array_equal(dec, d)
+
+
 @pytest.mark.parametrize("pb", [9, 10, 11])
 @pytest.mark.parametrize("seed", range(8))
 def test_normalize_bounds(pb, seed):
