@@ -1,15 +1,18 @@
 """Benchmark: encode+decode GB/s of the bf16 float codec on MI355X.
 
-Workload (BASELINE.json configs[1], "c2"): per GPU a batch of 256 x 1 MiB
-bf16 tensors (524,288 words each), N(0,1) fp32 truncated to bf16, seeded.
+N = 1 (headline, BASELINE.json configs[1], "c2"): a batch of 256 x 1 MiB bf16
+tensors (524,288 words each), N(0,1) fp32 truncated to bf16, seeded.
+N > 1 (BASELINE.json configs[4], "c5"): a FIXED batch of 8192 x 1 MiB bf16
+tensors sharded by contiguous element ranges, 8192 / N per rank (strong
+scaling; the tensors' contents do not depend on N).
+
 One step = floatCompress (pointer API, the reference's drop-in path) ->
 RCCL all-gather of the per-tensor compressed sizes (N > 1) -> floatDecompress.
-Weak scaling: every rank processes its own 256-tensor shard.
 
-value = N * U / step_time  (U = 256 MiB of uncompressed input per rank,
-GB/s = 1e9 B/s, reference convention benchmark.py:158-159).
+value = (uncompressed bytes of the whole batch) / max over ranks of the step
+time  (GB/s = 1e9 B/s, reference convention benchmark.py:158-159).
 
-Run:  python bench.py [--gpus N --steps K --warmup W]
+Run:  python bench.py [--gpus N --steps K --warmup W] [--workload c2|c5]
       torchrun --nproc-per-node N bench.py --gpus N ...
 """
 import argparse
@@ -33,7 +36,10 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=5)
-    p.add_argument("--batch", type=int, default=256)
+    p.add_argument("--workload", choices=("auto", "c2", "c5"), default="auto",
+                   help="auto: c2 at N=1, c5 (fixed 8192-tensor batch, sharded) at N>1")
+    p.add_argument("--batch", type=int, default=256, help="c2 tensors per GPU")
+    p.add_argument("--c5-batch", type=int, default=8192, help="c5 tensors in the whole job")
     p.add_argument("--words", type=int, default=524288)
     p.add_argument("--prob-bits", type=int, default=10)
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -68,12 +74,23 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
 
-    nb, n, pb = args.batch, args.words, args.prob_bits
+    n, pb = args.words, args.prob_bits
+    workload = args.workload if args.workload != "auto" else ("c2" if world == 1 else "c5")
+    if workload == "c5":
+        total = args.c5_batch
+        if total % world:
+            raise SystemExit(f"c5: {total} tensors do not shard evenly over {world} ranks")
+        first, last = D.shard_range(total, rank, world)
+        nb = last - first
+        x = _bf16_rows(first, last, n, dev)
+    else:
+        nb = args.batch
+        total = nb * world
+        g = torch.Generator(device=dev).manual_seed(1000 + rank)
+        x32 = torch.randn(nb, n, generator=g, device=dev, dtype=torch.float32)
+        x = (x32.view(torch.int32) >> 16).to(torch.int16).view(torch.bfloat16)  # truncation
+        del x32
     U = nb * n * 2  # bytes per rank
-    g = torch.Generator(device=dev).manual_seed(1000 + rank)
-    x32 = torch.randn(nb, n, generator=g, device=dev, dtype=torch.float32)
-    x = (x32.view(torch.int32) >> 16).to(torch.int16).view(torch.bfloat16)  # truncation
-    del x32
     L = N.lib()
     ft = 2
     cols = L.dietgpu_get_max_float_compressed_size(ft, n)
@@ -95,7 +112,7 @@ def main():
         N.check(L.dietgpu_float_compress(ws.h, ft, pb, 0, nb, in_ptrs, in_size, comp_ptrs,
                                          sizes.data_ptr(), stream))
         if world > 1:  # the only exchange: per-element compressed sizes (RCCL)
-            D.gather_sizes(sizes, nb * world)
+            D.gather_sizes(sizes, total)
         N.check(L.dietgpu_float_decompress(ws.h, ft, pb, 0, nb, comp_ptrs, out_ptrs, caps,
                                            ok.data_ptr(), osz.data_ptr(), stream))
 
@@ -158,7 +175,7 @@ def main():
     else:
         comp_total = comp_bytes
     ms_per_step = elapsed / args.steps * 1e3
-    value = world * U * args.steps / elapsed / 1e9
+    value = total * n * 2 * args.steps / elapsed / 1e9
     live = query_families()
     fam = dict(breakdown)
     if dominant in live:
@@ -180,13 +197,16 @@ def main():
     line = {
         "metric": METRIC, "value": round(value, 2), "unit": "GB/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+        "higher_is_better": True,
+        "scaling": "strong" if workload == "c5" else "weak", "vs_baseline": None, "dtype": "u32",
         "data": "synthetic",
-        "config": {"workload": f"c2: batch={nb} x {n * 2 // 1048576} MiB bf16 N(0,1) per GPU",
+        "config": {"workload": (f"c5: batch={total} x {n * 2 // 1048576} MiB bf16 N(0,1) in total, "
+                                f"{nb} per GPU" if workload == "c5" else
+                                f"c2: batch={nb} x {n * 2 // 1048576} MiB bf16 N(0,1) per GPU"),
                    "batch_per_gpu": nb, "words_per_tensor": n, "prob_bits": pb,
                    "api": "floatCompress + floatDecompress (pointer API, C ABI)",
                    "parallelism": f"dp{world} (independent shards + RCCL size all-gather)"},
-        "ratio": round(comp_total / (world * U), 5),
+        "ratio": round(comp_total / (total * n * 2), 5),
         "encode_plus_decode_algorithmic_GBps": (round(2 * (U + comp_bytes) / ((t_enc + t_dec) * 1e-3) / 1e9, 1)
                                                 if t_enc and t_dec else None),
         "compress_GBps_kernels": round(U / (t_enc * 1e-3) / 1e9, 1) if t_enc else None,
@@ -199,7 +219,7 @@ def main():
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = _cpu_baseline(x, min(args.cpu_sample, nb), pb)
-    if world == 1 and args.extras:
+    if world == 1 and workload == "c2" and args.extras:
         del comp, out, x, ws
         torch.cuda.empty_cache()
         line["extras"] = _extras(dev, pb)
@@ -207,6 +227,23 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def _bf16_rows(first, last, n, dev, chunk=512):
+    """Rows [first, last) of the c5 batch: N(0,1) fp32 truncated to bf16, the
+    rows of chunk c drawn from seed 5000 + c, so every row's contents are the
+    same whatever the sharding."""
+    import torch
+
+    x = torch.empty([last - first, n], dtype=torch.bfloat16, device=dev)
+    for c in range(first // chunk, -(-last // chunk)):
+        g = torch.Generator(device=dev).manual_seed(5000 + c)
+        x32 = torch.randn(chunk, n, generator=g, device=dev, dtype=torch.float32)
+        a, b = max(first, c * chunk), min(last, (c + 1) * chunk)
+        rows = (x32[a - c * chunk:b - c * chunk].view(torch.int32) >> 16).to(torch.int16)
+        x[a - first:b - first] = rows.view(torch.bfloat16)
+        del x32
+    return x
 
 
 def _timed(fn, reps):

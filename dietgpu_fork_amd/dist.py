@@ -63,10 +63,24 @@ class GpuFloatCodec:
 
 
 def _pack(comp, sizes, offs, length, dev):
+    """Pack the archive rows comp[i, :sizes[i]] back to back at the 16 B
+    aligned offsets `offs` (= archive_offsets(sizes)) into a buffer of
+    `length` bytes: one masked gather over the [nb, cols] archive matrix (the
+    16 B tails of each row ride along as don't-care padding), no per-element
+    launches."""
+    nb, cols = comp.shape
+    if cols % 16:
+        comp = torch.nn.functional.pad(comp, (0, 16 - cols % 16))
+        cols = comp.shape[1]
+    padded = ((sizes.to(torch.int64) + 15) // 16 * 16).to(comp.device)
+    if nb:
+        expect = torch.cumsum(padded.cpu(), 0) - padded.cpu()
+        assert torch.equal(expect, torch.as_tensor(offs, dtype=torch.int64).cpu()), \
+            "_pack: offsets must be the 16 B aligned exclusive prefix of the sizes"
     buf = torch.zeros(max(int(length), 16), dtype=torch.uint8, device=dev)
-    for i in range(len(sizes)):
-        o, s = int(offs[i]), int(sizes[i])
-        buf[o:o + s].copy_(comp[i, :s])
+    mask = torch.arange(cols, device=comp.device)[None, :] < padded[:, None]
+    flat = comp[mask]
+    buf[: flat.numel()] = flat.to(dev)
     return buf
 
 

@@ -7,6 +7,7 @@ import os
 import socket
 
 import numpy as np
+import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
@@ -144,3 +145,66 @@ def test_two_rank_gloo_compressed_collectives(tmp_path):
         for s in range(world):
             got = np.load(tmp_path / f"a2a{rank}_{s}.npy")
             assert np.array_equal(got, _a2a_input(s, rank).view(torch.int16).numpy()), (rank, s)
+
+
+C5_TOTAL, C5_WORDS = 64, 257  # the c5 plan at test size (bench.py: 8192 x 524288)
+
+
+def _c5_worker(rank, world, port, outdir):
+    """bench.py's N>1 leg minus the GPU: this rank's contiguous share of the
+    fixed batch (bench._bf16_rows), compressed locally (oracle standing in for
+    the GPU codec), per-element sizes all-gathered, max-over-ranks timing."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import bench
+        from dietgpu_fork_amd import dist as D
+        from oracle import oracle as O
+
+        first, last = D.shard_range(C5_TOTAL, rank, world)
+        assert last - first == C5_TOTAL // world
+        x = bench._bf16_rows(first, last, C5_WORDS, "cpu", chunk=16)
+        sizes = torch.tensor([O.float_compress(r.view(torch.int16).numpy().view(np.uint16), 2).size
+                              for r in x], dtype=torch.int32)
+        allsizes = D.gather_sizes(sizes, C5_TOTAL)
+        t = torch.tensor([float(rank + 1)], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        np.save(os.path.join(outdir, f"c5sizes{rank}.npy"), allsizes.numpy())
+        np.save(os.path.join(outdir, f"c5rows{rank}.npy"), x.view(torch.int16).numpy())
+        np.save(os.path.join(outdir, f"c5t{rank}.npy"), t.numpy())
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_c5_sharded_bench_plan(tmp_path, world):
+    """Every rank ends with the sizes of the whole fixed batch in element
+    order, the shards' rows are the unsharded batch's rows (the data does
+    not depend on the sharding), and the timing is the max over ranks."""
+    import bench
+    from oracle import oracle as O
+
+    mp.spawn(_c5_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    full = bench._bf16_rows(0, C5_TOTAL, C5_WORDS, "cpu", chunk=16)
+    ref = np.array([O.float_compress(r.view(torch.int16).numpy().view(np.uint16), 2).size for r in full])
+    rows = np.concatenate([np.load(tmp_path / f"c5rows{r}.npy") for r in range(world)])
+    assert np.array_equal(rows, full.view(torch.int16).numpy())
+    for r in range(world):
+        assert np.array_equal(np.load(tmp_path / f"c5sizes{r}.npy"), ref)
+        assert float(np.load(tmp_path / f"c5t{r}.npy")[0]) == world
+
+
+def test_pack_matches_per_element_copies():
+    from dietgpu_fork_amd import dist as D
+
+    g = torch.Generator().manual_seed(3)
+    comp = torch.randint(0, 256, (7, 100), generator=g, dtype=torch.uint8)
+    sizes = torch.tensor([0, 1, 15, 16, 17, 99, 100])
+    offs = D.archive_offsets(sizes)
+    length = int(offs[-1] + (sizes[-1] + 15) // 16 * 16) + 5
+    buf = D._pack(comp, sizes, offs, length, "cpu")
+    assert buf.numel() == length
+    for i in range(7):
+        o, s = int(offs[i]), int(sizes[i])
+        assert torch.equal(buf[o:o + s], comp[i, :s])
