@@ -447,7 +447,7 @@ static void checkOutAligned(const void* p, const char* what) {
 uint32_t getMaxCompressedSize(uint32_t bytes) {
   // ans/GpuANSEncode.cu:13-25 (overhead term evaluated for 4096 *blocks*)
   uint64_t raw = ansOverhead(kBlockSize);
-  raw += uint64_t(roundUp(kBlockSize + kBlockSize / 4, 16)) * divUp(bytes, kBlockSize);
+  raw += uint64_t(roundUp(kBlockSize + kBlockSize / 4, 16)) * ((uint64_t(bytes) + kBlockSize - 1) / kBlockSize);
   raw = roundUp64(raw, 16);
   DG_CHECK(raw <= uint64_t(INT32_MAX), "input too large: " << bytes << " bytes");
   return uint32_t(raw);

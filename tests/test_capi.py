@@ -118,3 +118,22 @@ def test_torch_ops_reject_cpu_tensors(N):
 
     with pytest.raises(RuntimeError):
         torch.ops.dietgpu.compress_data(True, [torch.zeros(16, dtype=torch.float16)])
+
+
+def test_oversize_requests_raise():
+    """Sizes whose archives cannot be described with 32-bit sizes raise
+    (the reference aborts: GpuANSEncode.cu:22 CHECK_LE) instead of returning
+    a bound the caller would allocate and overrun."""
+    import torch
+
+    import dietgpu_fork_amd  # noqa: F401
+    from dietgpu_fork_amd import codec as C
+    from dietgpu_fork_amd._native import DietGpuError
+
+    with pytest.raises(DietGpuError):
+        C.max_compressed_size(0xFFFFFFFF)
+    with pytest.raises(DietGpuError):
+        C.max_float_compressed_size(3, 1_000_000_000)
+    with pytest.raises(RuntimeError):
+        torch.ops.dietgpu.max_any_compressed_size(4_000_000_000)
+    assert C.max_float_compressed_size(2, 524288) == 1737280
