@@ -137,3 +137,27 @@ def test_oversize_requests_raise():
     with pytest.raises(RuntimeError):
         torch.ops.dietgpu.max_any_compressed_size(4_000_000_000)
     assert C.max_float_compressed_size(2, 524288) == 1737280
+
+
+def test_native_op_library_is_loaded(N):
+    """torch.ops.dietgpu comes from the native TORCH_LIBRARY library
+    (csrc/torch_ops.cpp), loaded like the reference's extension."""
+    import dietgpu_fork_amd  # noqa: F401
+    from dietgpu_fork_amd import ops
+
+    assert os.path.exists(ops.LIB_PATH)
+    ops.register()
+    maps = open("/proc/self/maps").read()
+    assert "libdietgpu_torch.so" in maps and "libdietgpu_amd.so" in maps
+    assert ops.max_any_compressed_size(4096) == torch.ops.dietgpu.max_any_compressed_size(4096)
+
+
+def test_cpp_api_program_links():
+    """tests/cpp/api_roundtrip.cpp (built by build()) links libdietgpu_amd.so
+    through include/dietgpu/*.h; without a GPU it reports so (exit 2)."""
+    import subprocess
+
+    exe = os.path.join(ROOT, "dietgpu_fork_amd", "_lib", "api_roundtrip")
+    assert os.path.exists(exe)
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=60)
+    assert r.returncode in (0, 2), r.stderr

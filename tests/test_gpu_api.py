@@ -347,3 +347,17 @@ def test_diff_positive_kat_archive(C, ws):
     ref = O.ans_encode(d, 10)
     assert osz.cpu().tolist() == [ref.size]
     np.testing.assert_array_equal(out[0, :ref.size].cpu().numpy(), ref)
+
+
+def test_cpp_api_program():
+    """A C++ program written against include/dietgpu/*.h only (no torch),
+    linked to libdietgpu_amd.so: pointer and split-size roundtrips of bytes
+    and all four float types, sizes and compressed-info readouts."""
+    import os
+    import subprocess
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = os.path.join(root, "dietgpu_fork_amd", "_lib", "api_roundtrip")
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=100)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert r.stdout.strip().endswith("OK")
