@@ -34,8 +34,8 @@ METRIC = "encode+decode GB/s (+ratio) on bf16 batch at 1/2/4/8 MI355X vs HBM roo
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=20)
-    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--steps", type=int, default=200)
+    p.add_argument("--warmup", type=int, default=20)
     p.add_argument("--workload", choices=("auto", "c2", "c5"), default="auto",
                    help="auto: c2 at N=1, c5 (fixed 8192-tensor batch, sharded) at N>1")
     p.add_argument("--batch", type=int, default=256, help="c2 tensors per GPU")

@@ -105,29 +105,11 @@ __device__ __forceinline__ uint32_t compOf(typename FloatTraits<FT>::WordT w, in
 // ---------------------------------------------------------------------------
 // reductions / scans for NT-thread workgroups (NT multiple of 64)
 // ---------------------------------------------------------------------------
+// Wave64 sum / inclusive scan on the VALU: DPP within rows of 16 lanes, then
+// v_readlane across the four rows -- no LDS-pipe shuffles (ds_bpermute),
+// whose round trips dominate these short latency-bound sequences.  Whole
+// wave (every lane active).
 __device__ __forceinline__ uint32_t waveSum(uint32_t v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-  return v;
-}
-__device__ __forceinline__ uint32_t waveXor(uint32_t v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v ^= __shfl_xor(v, o);
-  return v;
-}
-__device__ __forceinline__ uint32_t waveInclusiveScan(uint32_t v) {
-  const uint32_t lane = threadIdx.x & 63;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t u = __shfl_up(v, o);
-    if (lane >= uint32_t(o)) v += u;
-  }
-  return v;
-}
-// Wave64 sum / inclusive scan on the VALU (DPP within rows of 16 lanes, then
-// v_readlane across the four rows): no LDS-pipe shuffles (ds_bpermute),
-// whose round trips dominate short latency-bound sequences.
-__device__ __forceinline__ uint32_t waveSumDpp(uint32_t v) {
   v += uint32_t(__builtin_amdgcn_mov_dpp(int(v), 0xB1, 0xF, 0xF, true));   // quad_perm [1,0,3,2]
   v += uint32_t(__builtin_amdgcn_mov_dpp(int(v), 0x4E, 0xF, 0xF, true));   // quad_perm [2,3,0,1]
   v += uint32_t(__builtin_amdgcn_mov_dpp(int(v), 0x141, 0xF, 0xF, true));  // row_half_mirror
@@ -135,7 +117,12 @@ __device__ __forceinline__ uint32_t waveSumDpp(uint32_t v) {
   return uint32_t(__builtin_amdgcn_readlane(int(v), 0)) + uint32_t(__builtin_amdgcn_readlane(int(v), 16)) +
          uint32_t(__builtin_amdgcn_readlane(int(v), 32)) + uint32_t(__builtin_amdgcn_readlane(int(v), 48));
 }
-__device__ __forceinline__ uint32_t waveInclusiveScanDpp(uint32_t v) {
+__device__ __forceinline__ uint32_t waveXor(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v ^= __shfl_xor(v, o);
+  return v;
+}
+__device__ __forceinline__ uint32_t waveInclusiveScan(uint32_t v) {
   v += uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x111, 0xF, 0xF, true));  // row_shr:1
   v += uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x112, 0xF, 0xF, true));  // row_shr:2
   v += uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x114, 0xF, 0xF, true));  // row_shr:4

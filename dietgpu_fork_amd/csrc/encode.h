@@ -195,8 +195,9 @@ __device__ __forceinline__ uint32_t normalizeCount(uint32_t count, uint32_t tota
   const uint32_t qsum = blockSum<kThreads>(q, red);
 
   const int diff = int(W) - int(qsum);
-  uint32_t rank = kNumSymbols;
-  if (diff < 0) {
+  if (diff > 0) {
+    q += uint32_t(diff) / kNumSymbols + (s < uint32_t(diff) % kNumSymbols ? 1u : 0u);
+  } else if (diff < 0) {
     // Only entries with q > 1 are ever decremented, and they form a prefix
     // [0, g) of the descending key order, so a symbol's rank among the
     // (typically ~20) keys with q > 1 equals its rank in the full sort.
@@ -205,22 +206,41 @@ __device__ __forceinline__ uint32_t normalizeCount(uint32_t count, uint32_t tota
     const uint32_t pos = blockExclusiveScan<kThreads>(q > 1 ? 1u : 0u, red, &g0);
     if (q > 1) keys[pos] = key;
     __syncthreads();
+    uint32_t rank = kNumSymbols;
     if (q > 1) {
       rank = 0;
       for (uint32_t t = 0; t < g0; ++t) rank += keys[t] > key ? 1u : 0u;
     }
-  }
-  if (diff > 0) {
-    q += uint32_t(diff) / kNumSymbols + (s < uint32_t(diff) % kNumSymbols ? 1u : 0u);
-  } else if (diff < 0) {
-    int d = -diff;
-    while (d > 0) {
-      const int g = int(blockSum<kThreads>(q > 1 ? 1u : 0u, red));
-      if (g == 0) break;  // reference asserts; unreachable for real tables
-      const int k = d < g ? d : g;
-      if (int(rank) >= g - k && int(rank) < g) q -= 1;
-      d -= k;
+    __syncthreads();
+    if (q > 1) keys[rank] = q;  // the q > 1 values in rank order
+    __syncthreads();
+    if (threadIdx.x < 64) {
+      // the reference's rounds, on one wave: each takes 1 from the k = min(d,
+      // g) lowest-ranked of the g entries still > 1
+      const uint32_t lane = threadIdx.x;
+      uint32_t Q[kNumSymbols / 64];
+#pragma unroll
+      for (uint32_t j = 0; j < kNumSymbols / 64; ++j) Q[j] = lane + 64 * j < g0 ? keys[lane + 64 * j] : 1u;
+      int d = -diff;
+      while (d > 0) {
+        int g = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < kNumSymbols / 64; ++j) g += __popcll(ballot(Q[j] > 1));
+        if (g == 0) break;  // reference asserts; unreachable for real tables
+        const int k = d < g ? d : g;
+#pragma unroll
+        for (uint32_t j = 0; j < kNumSymbols / 64; ++j) {
+          const int r = int(lane + 64 * j);
+          if (r >= g - k && r < g) Q[j] -= 1;
+        }
+        d -= k;
+      }
+#pragma unroll
+      for (uint32_t j = 0; j < kNumSymbols / 64; ++j)
+        if (lane + 64 * j < g0) keys[lane + 64 * j] = Q[j];
     }
+    __syncthreads();
+    if (q > 1) q = keys[rank];
   }
   return q;
 }

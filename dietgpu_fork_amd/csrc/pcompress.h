@@ -65,7 +65,10 @@ constexpr uint32_t kSegSteps = 16;
 constexpr uint32_t kSegWords = kSegSteps * kLanesPerBlock;  // 512 symbols
 constexpr uint32_t kSegs = kSteps / kSegSteps;               // 8
 constexpr uint32_t kRing = 1024;  // u16 words per block ring (a typical block's whole output)
-constexpr uint32_t kSpill = 768;  // pending words that trigger a 256-word spill to the slot
+// pending words that trigger a 256-word spill to the slot: checked every
+// enc::kUnroll steps (<= 128 new words per block), so a block holds at most
+// kSpill + 127 < kRing unflushed words; most blocks never spill
+constexpr uint32_t kSpill = kRing - 128;
 // Largest team summed by every member (a 1 MiB-symbol element): its partials
 // are one sc1 load per member and bin.
 constexpr uint32_t kMaxTeam = 32;
@@ -142,12 +145,14 @@ __device__ __forceinline__ PItem itemOf(uint32_t i, const PCompArgs& a, const Ba
 // epoch reads as "not yet published".  Whole wave; returns the sum of the
 // values of members [0, x); `poison` in: this member's own, out: whether any
 // member [0, x] is poisoned (or the wait ran out of polls).
+// (storeOwn = false: this member's aggregate flag is already published)
 __device__ __forceinline__ uint32_t lookBackPoison(gp<uint64_t> f, uint32_t x, uint32_t agg,
-                                                   uint32_t epoch, uint32_t cap, bool& poison) {
+                                                   uint32_t epoch, uint32_t cap, bool& poison,
+                                                   bool storeOwn = true) {
   const uint32_t lane = laneId();
   const uint64_t tag = uint64_t(epoch) << 32;
   const uint64_t own = poison ? kFlagPoison : 0ull;
-  if (lane == 0)
+  if (storeOwn && lane == 0)
     __hip_atomic_store(f + x, (x == 0 ? kFlagPrefix : kFlagAgg) | own | tag | agg, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
   if (x == 0) return 0;
@@ -267,6 +272,7 @@ __global__ __launch_bounds__(pc::kThreads) __attribute__((amdgpu_waves_per_eu(4,
   for (uint32_t i = tid; i < pc::kHistWords / 4; i += pc::kThreads)
     *(lp<u32x4>)&hist[4 * i] = u32x4{0, 0, 0, 0};
   static_assert(pc::kHistWords % 4 == 0, "16 B zeroing");
+  static_assert(pc::kSpill + 32 * enc::kUnroll <= pc::kRing, "ring overflow between spill checks");
 
   // ---- per-item state (wave-uniform; E: encoding, L: loading) ----
   uint32_t symR[kRegs];
@@ -430,8 +436,8 @@ __global__ __launch_bounds__(pc::kThreads) __attribute__((amdgpu_waves_per_eu(4,
   };
 
   // ---- publish L's partial histogram, arrive ----
+  // (after a workgroup barrier: every wave's counts are in)
   auto publish = [&](const PItem& it) __attribute__((always_inline)) {
-    __syncthreads();  // every wave's counts are in
     uint32_t cnt = 0;
 #pragma unroll
     for (uint32_t k = 0; k < pc::kHistCols; ++k) {
@@ -498,6 +504,19 @@ __global__ __launch_bounds__(pc::kThreads) __attribute__((amdgpu_waves_per_eu(4,
     return timedOut;
   };
 
+  // ---- E's aggregate (its words, rounded to 8 per block) -> its look-back flag ----
+  auto publishAgg = [&](const PItem& it, bool poison) __attribute__((always_inline)) {
+    const uint32_t first = it.x * pc::kBlocksPerItem;
+    const uint32_t nk = first < it.nBlocks ? min(pc::kBlocksPerItem, it.nBlocks - first) : 0u;
+    const uint32_t r = lane < nk ? roundUp(cwE[lane], 8) : 0u;
+    const uint32_t agg = readfirst(__shfl(waveInclusiveScan(r), 63));
+    if (lane == 0)
+      __hip_atomic_store(G(A().flags) + it.tb + it.x,
+                         (it.x == 0 ? kFlagPrefix : kFlagAgg) | (poison ? kFlagPoison : 0ull) |
+                             (uint64_t(A().epoch) << 32) | agg,
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
+
   // ---- placement of E: look-back, headers, payload copy-out ----
   auto place = [&](const PItem& it, bool poison, uint32_t ckE) __attribute__((always_inline)) {
     // spilled words are read back by other waves of this workgroup: a wave
@@ -516,7 +535,7 @@ __global__ __launch_bounds__(pc::kThreads) __attribute__((amdgpu_waves_per_eu(4,
       const uint32_t inc = waveInclusiveScan(r);
       const uint32_t agg = readfirst(__shfl(inc, 63));
       bool pz = poison;
-      const uint32_t excl = lookBackPoison(G(A().flags) + it.tb, it.x, agg, A().epoch, A().spinCap, pz);
+      const uint32_t excl = lookBackPoison(G(A().flags) + it.tb, it.x, agg, A().epoch, A().spinCap, pz, false);
       if (lane < nk) preE[lane] = excl + inc - r;
       if (lane == 0 && it.x == it.team - 1) {
         if (pz) {
@@ -627,6 +646,7 @@ __global__ __launch_bounds__(pc::kThreads) __attribute__((amdgpu_waves_per_eu(4,
   while (true) {
     const bool hasE = iE < A().items, hasL = iL < A().items;
     if (!hasE && !hasL) break;
+    __builtin_amdgcn_s_setprio(0);
     {
       const PItem E = itemOf(iE, A(), IN()), L = itemOf(iL, A(), IN());
       const uint32_t uwE0 = pairSize(E, 0), uwE1 = pairSize(E, 1);
@@ -673,8 +693,15 @@ __global__ __launch_bounds__(pc::kThreads) __attribute__((amdgpu_waves_per_eu(4,
       }
       if (hasE) encodeDone(E);
     }
+    // The hand-offs below are on the team's critical path while the other
+    // workgroups of this CU stream: they issue at raised priority (3 % of
+    // the c2 launch, same-box A/B).
+    __builtin_amdgcn_s_setprio(2);
+    // E's word counts and L's histogram counts are in; E's aggregate goes out
+    // at once, so that the team's look-backs in place() rarely wait
+    __syncthreads();
+    if (hasE && w == 0) publishAgg(itemOf(iE, A(), IN()), poisonE);
     if (hasL) publish(itemOf(iL, A(), IN()));
-    else __syncthreads();
     if (hasE) place(itemOf(iE, A(), IN()), poisonE, ckE);
     uint32_t iN = A().items;
     if (hasL) {

@@ -9,7 +9,7 @@ cp "$LIB" /tmp/ab_default.so
 for L in "$@"; do
   T=$(basename "$L" .so)
   if [ "$L" = default ]; then cp /tmp/ab_default.so "$LIB"; else cp "$L" "$LIB"; fi
-  timeout -k 10 200 python3 -u bench.py --no-cpu-baseline --no-extras --no-verify > gpurun_out/ab_$T.log 2>&1 || exit 1
+  timeout -k 10 200 python3 -u bench.py --no-cpu-baseline --no-extras --no-verify --steps ${AB_STEPS:-20} > gpurun_out/ab_$T.log 2>&1 || exit 1
   python3 -c "
 import json
 for l in open('gpurun_out/ab_$T.log'):
