@@ -334,6 +334,48 @@ def _extras(dev, pb, reps=3):
                int(sizes.to(torch.int64).sum()), tc, td, exact, kernels_ms=kern)
         del x, y, arch, ws
 
+    # batch 1 x 128*512*1024 words (one large tensor):
+    # the whole batch is a single element, so it takes the three-kernel path
+    for dt in (torch.bfloat16, torch.float16, torch.float32):
+        words = 128 * 512 * 1024
+        g = torch.Generator(device=dev).manual_seed(13)
+        x = torch.randn(1, words, generator=g, device=dev).to(dt)
+        ws = C.Workspace(1 << 30, dev)
+        arch, sizes = C.float_compress_stride(x, prob_bits=pb, ws=ws)
+        y, ok, _ = C.float_decompress_stride(arch, words, dt, prob_bits=pb, ws=ws)
+        tc = _timed(lambda: C.float_compress_stride(x, prob_bits=pb, ws=ws, out=arch, sizes=sizes), reps)
+        td = _timed(lambda: C.float_decompress_stride(arch, words, dt, prob_bits=pb, ws=ws, out=y), reps)
+        exact = bool((ok == 1).all()) and torch.equal(x.view(torch.uint8), y.view(torch.uint8))
+        kern = breakdown(lambda: C.float_compress_stride(x, prob_bits=pb, ws=ws, out=arch, sizes=sizes),
+                         lambda: C.float_decompress_stride(arch, words, dt, prob_bits=pb, ws=ws, out=y))
+        record(f"batch 1 x 128*512*1024 {str(dt)[6:]} N(0,1) (one element)", x.numel() * x.element_size(),
+               int(sizes.to(torch.int64).sum()), tc, td, exact, kernels_ms=kern)
+        del x, y, arch, ws
+        torch.cuda.empty_cache()
+
+    # per-call latency of the torch ops (host validation + launch) on a small
+    # batch: 8 x 4096 bf16, the kernels themselves take a few microseconds
+    xs = [torch.randn(4096, device=dev).to(torch.bfloat16) for _ in range(8)]
+    tmp = torch.empty([64 << 20], dtype=torch.uint8, device=dev)
+    comp, csz, _ = torch.ops.dietgpu.compress_data(True, xs, False, tmp)
+    rows = [comp[i, : int(csz[i])] for i in range(len(xs))]
+    outs = [torch.empty_like(t) for t in xs]
+    lat = {}
+    for name, fn in (("compress_data", lambda: torch.ops.dietgpu.compress_data(True, xs, False, tmp)),
+                     ("decompress_data", lambda: torch.ops.dietgpu.decompress_data(True, rows, outs, False, tmp))):
+        for _ in range(20):
+            fn()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(200):
+            fn()
+        t_host = (time.perf_counter() - t0) / 200
+        torch.cuda.synchronize()
+        t_all = (time.perf_counter() - t0) / 200
+        lat[name] = {"host_us_per_call": round(t_host * 1e6, 2), "us_per_call_synced": round(t_all * 1e6, 2)}
+    out.append({"config": "torch.ops.dietgpu per-call latency, 8 x 4096 bf16, 64 MiB temp_mem", **lat})
+    del xs, tmp, comp, rows, outs
+
     # c4: fp64 two-pass (16,777,216 words) and 90 %-sparse fp32 (15,000,000)
     g = torch.Generator(device=dev).manual_seed(4)
     x = torch.randn(16777216, generator=g, device=dev, dtype=torch.float64)

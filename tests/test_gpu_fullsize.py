@@ -63,3 +63,23 @@ def test_c5_single_gpu(C):
         ref = O.float_compress(x[i].view(torch.int16).cpu().numpy().view(np.uint16), 2)
         assert s[i] == ref.size, i
         np.testing.assert_array_equal(arch[i, : ref.size].cpu().numpy(), ref, err_msg=f"element {i}")
+
+
+@pytest.mark.parametrize("dtype,ft", [(torch.bfloat16, 2), (torch.float16, 1), (torch.float32, 3)])
+def test_batch1_large_tensor(C, dtype, ft):
+    """One 128*512*1024-word tensor (a single element of 64 M words, the
+    three-kernel path): bit-exact roundtrip and an archive byte-identical to
+    the oracle's."""
+    words = 128 * 512 * 1024
+    g = torch.Generator(device=DEV).manual_seed(13)
+    x = torch.randn(1, words, generator=g, device=DEV).to(dtype)
+    ws = C.Workspace(1 << 30)
+    arch, sizes = C.float_compress_stride(x, prob_bits=10, ws=ws)
+    s = int(sizes[0])
+    iw = torch.int16 if x.element_size() == 2 else torch.int32
+    ref = O.float_compress(x[0].view(iw).cpu().numpy().view(np.uint16 if iw == torch.int16 else np.uint32), ft)
+    assert s == ref.size and s % 16 == 0
+    np.testing.assert_array_equal(arch[0, :s].cpu().numpy(), ref)
+    out, ok, osz = C.float_decompress_stride(arch, words, dtype, prob_bits=10, ws=ws)
+    assert int(ok[0]) == 1 and int(osz[0]) == words
+    assert torch.equal(out.view(iw), x.view(iw))
