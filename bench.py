@@ -188,7 +188,7 @@ def main():
     roofline = None
     if dominant:
         ach = algo[dominant] / (fam[dominant]["avg_ms"] * 1e-3) / 1e9
-        roofline = {"bound": "hbm", "kernel": f"k_{dominant}", "achieved": round(ach, 1),
+        roofline = {"bound": "hbm", "kernel": KERNEL_OF[dominant], "achieved": round(ach, 1),
                     "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBPS, 4),
                     "traffic": _pmc_traffic(dominant, ft),
                     "algorithmic_bytes_per_launch": algo[dominant]}
@@ -408,6 +408,11 @@ def _extras(dev, pb, reps=3):
     return out
 
 
+# profiling family (csrc/profile.h scopes) -> kernel symbol
+KERNEL_OF = {"compress": "k_pcompress", "hist": "k_hist", "normalize": "k_normalize", "encode": "k_encode",
+             "coalesce": "k_coalesce", "decode": "k_decode", "sparse": "k_sparse"}
+
+
 def _pmc_traffic(kernel, ft):
     """HBM bytes per launch of `kernel`'s instance for float type `ft` from
     the newest committed rocprofv3 PMC summary (profiles/*pmc*.json, written
@@ -422,7 +427,7 @@ def _pmc_traffic(kernel, ft):
         except Exception:
             continue
         for name, k in d.get("kernels", {}).items():
-            if name.startswith(f"k_{kernel}<{ft},") and "hbm_bytes_per_launch" in k:
+            if name.startswith(f"{KERNEL_OF[kernel]}<{ft},") and "hbm_bytes_per_launch" in k:
                 return k["hbm_bytes_per_launch"]
     return None
 
