@@ -31,4 +31,8 @@ std::vector<std::pair<int, std::string>> verifyChecksums(StackDeviceMemory& res,
                                                          uint32_t maxBytes, hipStream_t s,
                                                          const DeviceTables* tabs = nullptr);
 
+// The device error word (elements whose compression was abandoned after a
+// bounded wait ran out; their outSize is 0), codec.hip.
+uint32_t* deviceErrorWord();
+
 }  // namespace dietgpu

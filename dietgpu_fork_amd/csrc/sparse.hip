@@ -5,8 +5,10 @@
 // float/GpuSparseFloatDecompress.{cu,cuh}.  The reference scans with one
 // thrust::exclusive_scan per batch element on the legacy default stream
 // between two cudaDeviceSynchronize calls (GpuSparseFloatCompress.cuh:360-369);
-// here the scan is a batched two-level scan over 4096-word tiles, fully
-// stream-ordered (no host or device-wide sync).
+// here compression is ONE pass over the input (k_sparseCompress: bitmap, tile
+// counts, decoupled look-back over the tiles of an element, compaction), and
+// decompression scans the bitmap's tile popcounts, fully stream-ordered (no
+// host or device-wide sync).
 //
 // Wire format: 16 B header {u32 N, 12 B zero}, bitmap
 // ceil(N/8) bytes (bit 7 of byte k <-> element 8k) padded to 16, then a dense
@@ -22,7 +24,9 @@
 #include "dietgpu/GpuFloatCodec.h"
 #include "decode.h"
 #include "encode.h"
+#include "lookback.h"
 #include "profile.h"
+#include "sync_arena.h"
 
 namespace dietgpu {
 
@@ -44,224 +48,263 @@ __device__ __forceinline__ bool isNonzero(WordOf<FT> w) {
   return w != 0;  // bitwise: -0.0 is "nonzero" (generate_bitmap :56)
 }
 
-// s1: bitmap + per-tile nonzero count.  grid (tiles, batch)
-template <int FT>
-__global__ __launch_bounds__(kThreads) void k_sparseBitmap(BatchDesc in, const uint64_t* outPtrs,
-                                                           uint32_t batchOffset,
-                                                           uint32_t tilesPerElem,
-                                                           uint32_t* __restrict__ tileCounts) {
-  __shared__ uint32_t red[kWaves];
-  const uint32_t b = batchOffset + blockIdx.y;
-  const uint32_t n = in.size(b);
-  const uint32_t tile = blockIdx.x;
-  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const WordOf<FT>* x = reinterpret_cast<const WordOf<FT>*>(in.start(b));
-  uint8_t* o = reinterpret_cast<uint8_t*>(outPtrs[b]);
-  const uint32_t bmBytes = (n + 7) / 8, bmPad = roundUp(bmBytes, 16);
-  if (tile == 0 && threadIdx.x == 0) {
-    reinterpret_cast<uint4*>(o)[0] = make_uint4(n, 0, 0, 0);
-  }
-  uint32_t cnt = 0;
-  const uint32_t base = tile * kTileWords + w * (kTileWords / kWaves);
-  if (base < n) {
-#pragma unroll 4
-    for (uint32_t j = 0; j < kTileWords / kWaves / 64; ++j) {
-      const uint32_t i0 = base + 64 * j;
-      if (i0 >= n) break;
-      const uint32_t i = i0 + lane;
-      const bool f = i < n && isNonzero<FT>(x[i]);
-      const uint64_t m = ballot(f);
-      cnt += uint32_t(__popcll(m));
-      if (lane == 0) {
-        uint64_t* dst = reinterpret_cast<uint64_t*>(o + 16 + i0 / 8);
-        dst[0] = maskToBitmap(m);
-        // zero the 16-byte padding after the last bitmap word
-        const uint32_t end = i0 / 8 + 8;
-        if (i0 + 64 >= n && end < bmPad) dst[1] = 0;
-      }
-    }
-  }
-  cnt = blockSum<kThreads>(lane == 0 ? cnt : 0u, red);
-  if (threadIdx.x == 0) tileCounts[uint64_t(b) * tilesPerElem + tile] = cnt;
-}
-
-// s2 / d2: exclusive scan of tile counts per element (in place); optional
-// compacted-list length with the n-2 quirk.  grid (batch)
-template <int FT>
-__global__ __launch_bounds__(kThreads) void k_sparseScan(BatchDesc in, uint32_t batchOffset,
-                                                         uint32_t tilesPerElem,
-                                                         const uint32_t* __restrict__ sizes,
-                                                         uint32_t* __restrict__ tileCounts,
-                                                         uint32_t* __restrict__ listLen) {
-  __shared__ uint32_t red[kWaves];
-  const uint32_t b = batchOffset + blockIdx.x;
-  const uint32_t n = sizes ? sizes[b] : in.size(b);
-  const uint32_t tiles = min(divUp(n, kTileWords), tilesPerElem);
-  uint32_t* tc = tileCounts + uint64_t(b) * tilesPerElem;
-  uint32_t carry = 0;
-  for (uint32_t t0 = 0; t0 < tiles; t0 += kThreads) {
-    const uint32_t t = t0 + threadIdx.x;
-    const uint32_t v = t < tiles ? tc[t] : 0u;
-    uint32_t total = 0;
-    const uint32_t ex = blockExclusiveScan<kThreads>(v, red, &total);
-    if (t < tiles) tc[t] = carry + ex;
-    carry += total;
-    __syncthreads();
-  }
-  if (listLen && threadIdx.x == 0) {
-    const WordOf<FT>* x = reinterpret_cast<const WordOf<FT>*>(in.start(b));
-    uint32_t len = 0;
-    if (n == 1) {
-      len = isNonzero<FT>(x[0]) ? 1u : 0u;
-    } else if (n >= 2) {
-      // idx[n-2] + flag[n-1] + 1 == nnz - flag[n-2] + 1
-      len = carry - (isNonzero<FT>(x[n - 2]) ? 1u : 0u) + 1u;
-    }
-    listLen[b] = len;
-  }
-}
-
-// s3: scatter nonzeros into the compacted list.  grid (tiles, batch)
-template <int FT>
-__global__ __launch_bounds__(kThreads) void k_sparseCompact(BatchDesc in, uint32_t batchOffset,
-                                                            uint32_t tilesPerElem,
-                                                            const uint32_t* __restrict__ tileOff,
-                                                            const uint64_t* __restrict__ listPtrs) {
+// Compression in one pass.  grid (tiles, batch); a workgroup takes one
+// 4096-word tile of one element: it loads the tile (16 B vectors when the
+// element is 16 B aligned, coalesced) into LDS, then each wave takes 1024
+// consecutive words as 16 steps of 64 lanes: the ballot of nonzero flags is
+// the step's 64 bitmap bits (generate_bitmap :40-71) and its nonzeros'
+// ranks (v_mbcnt).  The tile's nonzero count goes through a decoupled
+// look-back over the element's earlier tiles (epoch-tagged flags, lookback.h);
+// then the nonzeros are scattered into the compacted list (fill_comp_input
+// :119-185, n-2 quirk included).  A look-back that runs out of polls marks the
+// element (its final outSize becomes 0) instead of guessing.
+template <int FT, bool kVec>
+__global__ __launch_bounds__(kThreads) void k_sparseCompress(BatchDesc in, const uint64_t* outPtrs,
+                                                             uint32_t batchOffset, uint32_t tilesPerElem,
+                                                             const uint64_t* __restrict__ listPtrs,
+                                                             uint32_t* __restrict__ listLen,
+                                                             uint64_t* __restrict__ flags, uint32_t epoch,
+                                                             uint32_t spinCap, uint8_t* __restrict__ poisoned,
+                                                             uint32_t* __restrict__ err) {
+  using W = WordOf<FT>;
   constexpr uint32_t kSteps = kTileWords / kWaves / 64;
+  constexpr uint32_t kVecs = kTileWords * sizeof(W) / 16 / kThreads;  // 16 B vectors per thread
+  __shared__ __attribute__((aligned(16))) W buf[kTileWords];
   __shared__ uint32_t waveCnt[kWaves];
+  __shared__ uint32_t exclS;
+  __shared__ uint32_t poisonS;
   const uint32_t b = batchOffset + blockIdx.y;
   const uint32_t n = in.size(b);
   const uint32_t tile = blockIdx.x;
-  if (tile * kTileWords >= n) return;
-  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const WordOf<FT>* x = reinterpret_cast<const WordOf<FT>*>(in.start(b));
-  WordOf<FT>* list = reinterpret_cast<WordOf<FT>*>(listPtrs[b]);
-  const uint32_t base = tile * kTileWords + w * (kTileWords / kWaves);
-  WordOf<FT> v[kSteps];
+  if (tile * kTileWords >= n && !(n == 0 && tile == 0)) return;
+  const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  gp<const W> x = (gp<const W>)in.start(b);
+  gp<uint8_t> o = (gp<uint8_t>)outPtrs[b];
+  if (tile == 0 && tid == 0) st16(o, make_uint4(n, 0, 0, 0));
+  const uint32_t t0 = tile * kTileWords;
+  const uint32_t tileN = min(kTileWords, n - min(n, t0));
+  // tile -> LDS (words past the element read as 0)
+  if (kVec) {
+    constexpr uint32_t kWPV = 16 / sizeof(W);
+#pragma unroll
+    for (uint32_t v = 0; v < kVecs; ++v) {
+      const uint32_t wi = (v * kThreads + tid) * kWPV;  // first word of the vector
+      uint4 val = make_uint4(0, 0, 0, 0);
+      if (wi + kWPV <= tileN) {
+        val = ld16((gp<const uint4>)(x + t0 + wi));
+      } else if (wi < tileN) {
+        W tmp[kWPV];
+#pragma unroll
+        for (uint32_t k = 0; k < kWPV; ++k) tmp[k] = wi + k < tileN ? x[t0 + wi + k] : W(0);
+        __builtin_memcpy(&val, tmp, 16);
+      }
+      *(lp<u32x4>)&buf[wi] = u32x4{val.x, val.y, val.z, val.w};
+    }
+  } else {
+#pragma unroll 4
+    for (uint32_t i = tid; i < kTileWords; i += kThreads) buf[i] = i < tileN ? x[t0 + i] : W(0);
+  }
+  __syncthreads();
+  // bitmap bits and counts, wave w: words [w * 1024, (w + 1) * 1024) of the tile
+  const uint32_t bmBytes = (n + 7) / 8, bmPad = roundUp(bmBytes, 16);
   uint64_t m[kSteps];
   uint32_t cnt = 0;
 #pragma unroll
   for (uint32_t j = 0; j < kSteps; ++j) {
-    const uint32_t i = base + 64 * j + lane;
-    v[j] = i < n ? x[i] : WordOf<FT>(0);
-    m[j] = ballot(v[j] != 0);
+    const uint32_t q = w * (kTileWords / kWaves) + 64 * j;  // step's first word in the tile
+    m[j] = ballot(buf[q + lane] != W(0));  // bitwise: -0.0 is "nonzero" (generate_bitmap :56)
     cnt += uint32_t(__popcll(m[j]));
+    const uint32_t i0 = t0 + q;
+    if (lane == 0 && i0 < n) {
+      gp<uint64_t> dst = (gp<uint64_t>)(o + 16 + i0 / 8);
+      dst[0] = maskToBitmap(m[j]);
+      // zero the 16-byte padding after the last bitmap word
+      const uint32_t end = i0 / 8 + 8;
+      if (i0 + 64 >= n && end < bmPad) dst[1] = 0;
+    }
   }
   if (lane == 0) waveCnt[w] = cnt;
   __syncthreads();
-  uint32_t pos = tileOff[uint64_t(b) * tilesPerElem + tile];
+  if (w == 0) {
+    const uint32_t total = waveCnt[0] + waveCnt[1] + waveCnt[2] + waveCnt[3];
+    bool pz = false;
+    const uint32_t excl =
+        lookBackPoison(G(flags) + uint64_t(b) * tilesPerElem, tile, total, epoch, spinCap, pz);
+    if (lane == 0) {
+      exclS = excl;
+      poisonS = pz ? 1u : 0u;
+      if ((tile + 1) * kTileWords >= n) {  // the element's last tile
+        uint32_t len = 0;
+        if (n == 1) {
+          len = buf[0] != W(0) ? 1u : 0u;
+        } else if (n >= 2) {
+          // idx[n-2] + flag[n-1] + 1 == nnz - flag[n-2] + 1
+          len = excl + total - (x[n - 2] != W(0) ? 1u : 0u) + 1u;
+        }
+        listLen[b] = pz ? 0u : len;
+        poisoned[b] = pz ? 1 : 0;
+        if (pz) __hip_atomic_fetch_add(G(err), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
+  __syncthreads();
+  if (poisonS) return;
+  uint32_t pos = exclS;
   for (uint32_t k = 0; k < w; ++k) pos += waveCnt[k];
+  gp<W> list = (gp<W>)listPtrs[b];
   // the n-2 quirk: x[n-1] goes to idx[n-2] + 1 and, when x[n-2] == 0, the
   // skipped slot idx[n-2] is part of the list (written as 0)
-  const bool gap = n >= 2 && x[n - 2] == 0;
+  const bool gap = n >= 2 && x[n - 2] == W(0);
 #pragma unroll
   for (uint32_t j = 0; j < kSteps; ++j) {
-    const uint32_t i = base + 64 * j + lane;
+    const uint32_t q = w * (kTileWords / kWaves) + 64 * j + lane;
+    const uint32_t i = t0 + q;
+    const W v = buf[q];
     const uint32_t dst = pos + mbcnt(m[j]);
     if (i + 1 == n && gap) {
-      list[dst] = WordOf<FT>(0);
-      if (v[j] != 0) list[dst + 1] = v[j];
-    } else if (v[j] != 0) {
-      list[dst] = v[j];
+      list[dst] = W(0);
+      if (v != W(0)) list[dst + 1] = v;
+    } else if (v != W(0)) {
+      list[dst] = v;
     }
     pos += uint32_t(__popcll(m[j]));
   }
 }
 
-__global__ void k_sparseAddSizes(BatchDesc in, uint32_t numInBatch, uint32_t* __restrict__ outSize) {
+// outSize of the sparse archive: header + padded bitmap + dense archive; 0 for
+// an element whose compaction was abandoned (k_sparseCompress)
+__global__ void k_sparseAddSizes(BatchDesc in, uint32_t numInBatch, const uint8_t* __restrict__ poisoned,
+                                 uint32_t* __restrict__ outSize) {
   const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b < numInBatch && outSize) outSize[b] += 16 + roundUp((in.size(b) + 7) / 8, 16);
+  if (b < numInBatch && outSize)
+    outSize[b] = poisoned[b] ? 0u : outSize[b] + 16 + roundUp((in.size(b) + 7) / 8, 16);
 }
 
-// d1: headers -> dense-archive pointers + per-tile popcounts of the bitmap.
-// grid (tiles, batch)
-__global__ __launch_bounds__(kThreads) void k_sparseHeaders(BatchDesc in, uint32_t batchOffset,
-                                                            uint32_t tilesPerElem,
-                                                            uint64_t* __restrict__ densePtrs,
-                                                            uint32_t* __restrict__ sizes,
-                                                            uint32_t* __restrict__ tileCounts) {
-  __shared__ uint32_t red[kWaves];
-  const uint32_t b = batchOffset + blockIdx.y;
+// d1: headers -> dense-archive pointers and sizes.  One thread per element.
+__global__ void k_sparseHeaders(BatchDesc in, uint32_t numInBatch, uint64_t* __restrict__ densePtrs,
+                                uint32_t* __restrict__ sizes) {
+  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= numInBatch) return;
   const uint8_t* a = in.start(b);
   const uint32_t n = reinterpret_cast<const uint32_t*>(a)[0];
-  const uint32_t tile = blockIdx.x;
-  if (tile == 0 && threadIdx.x == 0) {
-    densePtrs[b] = reinterpret_cast<uint64_t>(a + 16 + roundUp((n + 7) / 8, 16));
-    sizes[b] = n;
-  }
-  if (tile >= tilesPerElem) return;
-  uint32_t c = 0;
-  const uint32_t bytes0 = tile * (kTileWords / 8);
-  const uint32_t bmBytes = (n + 7) / 8;
-  for (uint32_t k = threadIdx.x; k < kTileWords / 8; k += kThreads) {
-    if (bytes0 + k < bmBytes) c += __popc(a[16 + bytes0 + k]);
-  }
-  c = blockSum<kThreads>(c, red);
-  if (threadIdx.x == 0) tileCounts[uint64_t(b) * tilesPerElem + tile] = c;
+  densePtrs[b] = reinterpret_cast<uint64_t>(a + 16 + roundUp((n + 7) / 8, 16));
+  sizes[b] = n;
 }
 
-// d3: expand the decoded nonzero list into the output.  grid (tiles, batch)
-template <int FT>
-__global__ __launch_bounds__(kThreads) void k_sparseExpand(BatchDesc in, BatchDesc out,
-                                                           uint32_t batchOffset,
-                                                           uint32_t tilesPerElem,
-                                                           const uint32_t* __restrict__ sizes,
-                                                           const uint32_t* __restrict__ tileOff,
+// d3: expand the decoded nonzero list into the output (fill_in_nonzeros
+// :95-144).  grid (tiles, batch); per 4096-word tile: the bitmap's popcount,
+// a decoupled look-back over the element's earlier tiles for the tile's
+// first list index, the expansion into LDS, and 16 B stores when the output
+// is 16 B aligned.  The element's last tile reports success and size (a
+// look-back that runs out of polls reports failure).
+template <int FT, bool kVec>
+__global__ __launch_bounds__(kThreads) void k_sparseExpand(BatchDesc in, BatchDesc out, uint32_t batchOffset,
+                                                           uint32_t tilesPerElem, const uint32_t* __restrict__ sizes,
                                                            const uint64_t* __restrict__ listPtrs,
                                                            const uint8_t* __restrict__ denseOk,
                                                            uint8_t* __restrict__ outSuccess,
-                                                           uint32_t* __restrict__ outSize) {
+                                                           uint32_t* __restrict__ outSize, uint64_t* __restrict__ flags,
+                                                           uint32_t epoch, uint32_t spinCap,
+                                                           uint32_t* __restrict__ err) {
+  using W = WordOf<FT>;
   constexpr uint32_t kSteps = kTileWords / kWaves / 64;
+  constexpr uint32_t kVecs = kTileWords * sizeof(W) / 16 / kThreads;
+  __shared__ __attribute__((aligned(16))) W buf[kTileWords];
   __shared__ uint32_t waveCnt[kWaves];
+  __shared__ uint32_t exclS, poisonS;
   const uint32_t b = batchOffset + blockIdx.y;
   const uint32_t n = sizes[b];
   const bool ok = denseOk[b] != 0 && out.size(b) >= n;
   const uint32_t tile = blockIdx.x;
-  if (tile == 0 && threadIdx.x == 0) {
-    if (outSuccess) outSuccess[b] = ok ? 1 : 0;
-    if (outSize) outSize[b] = n;  // fill_in_nonzeros :107-109
+  const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  if (n == 0) {
+    if (tile == 0 && tid == 0) {
+      if (outSuccess) outSuccess[b] = ok ? 1 : 0;
+      if (outSize) outSize[b] = 0;
+    }
+    return;
   }
-  if (!ok || tile * kTileWords >= n) return;
-  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const uint8_t* bm = in.start(b) + 16;
-  const WordOf<FT>* list = reinterpret_cast<const WordOf<FT>*>(listPtrs[b]);
-  WordOf<FT>* y = reinterpret_cast<WordOf<FT>*>(out.start(b));
-  const uint32_t base = tile * kTileWords + w * (kTileWords / kWaves);
+  if (tile * kTileWords >= n) return;
+  const bool last = (tile + 1) * kTileWords >= n;
+  if (!ok) {
+    if (last && tid == 0) {
+      if (outSuccess) outSuccess[b] = 0;
+      if (outSize) outSize[b] = n;  // fill_in_nonzeros :107-109
+    }
+    return;
+  }
+  gp<const uint8_t> bm = (gp<const uint8_t>)in.start(b) + 16;
+  const uint32_t t0 = tile * kTileWords;
   uint64_t m[kSteps];
   uint32_t cnt = 0;
 #pragma unroll
   for (uint32_t j = 0; j < kSteps; ++j) {
-    const uint32_t i0 = base + 64 * j;
-    m[j] = i0 < n ? maskToBitmap(*reinterpret_cast<const uint64_t*>(bm + i0 / 8)) : 0ull;
+    const uint32_t i0 = t0 + w * (kTileWords / kWaves) + 64 * j;
+    m[j] = i0 < n ? maskToBitmap(*(gp<const uint64_t>)(bm + i0 / 8)) : 0ull;
     if (i0 < n && n - i0 < 64) m[j] &= (1ull << (n - i0)) - 1;
     cnt += uint32_t(__popcll(m[j]));
   }
   if (lane == 0) waveCnt[w] = cnt;
   __syncthreads();
-  uint32_t pos = tileOff[uint64_t(b) * tilesPerElem + tile];
+  if (w == 0) {
+    bool pz = false;
+    const uint32_t total = waveCnt[0] + waveCnt[1] + waveCnt[2] + waveCnt[3];
+    const uint32_t excl =
+        lookBackPoison(G(flags) + uint64_t(b) * tilesPerElem, tile, total, epoch, spinCap, pz);
+    if (lane == 0) {
+      exclS = excl;
+      poisonS = pz ? 1u : 0u;
+      if (last) {
+        if (outSuccess) outSuccess[b] = pz ? 0 : 1;
+        if (outSize) outSize[b] = n;
+        if (pz) __hip_atomic_fetch_add(G(err), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
+  __syncthreads();
+  if (poisonS) return;
+  uint32_t pos = exclS;
   for (uint32_t k = 0; k < w; ++k) pos += waveCnt[k];
+  gp<const W> list = (gp<const W>)listPtrs[b];
   // x[n-1] is read from idx[n-2] + 1 (fill_in_nonzeros :139-144)
   const bool gap = n >= 2 && ((bm[(n - 2) / 8] >> (7 - (n - 2) % 8)) & 1) == 0;
 #pragma unroll
   for (uint32_t j = 0; j < kSteps; ++j) {
-    const uint32_t i = base + 64 * j + lane;
-    if (i < n) {
-      const bool f = (m[j] >> lane) & 1;
-      uint32_t src = pos + mbcnt(m[j]);
-      if (i + 1 == n && gap) src += 1;
-      y[i] = f ? list[src] : WordOf<FT>(0);
-    }
+    const uint32_t q = w * (kTileWords / kWaves) + 64 * j + lane;
+    const uint32_t i = t0 + q;
+    const bool f = (m[j] >> lane) & 1;
+    uint32_t src = pos + mbcnt(m[j]);
+    if (i + 1 == n && gap) src += 1;
+    buf[q] = f ? list[src] : W(0);
     pos += uint32_t(__popcll(m[j]));
+  }
+  __syncthreads();
+  gp<W> y = (gp<W>)out.start(b);
+  const uint32_t tileN = min(kTileWords, n - t0);
+  if (kVec) {
+    constexpr uint32_t kWPV = 16 / sizeof(W);
+#pragma unroll
+    for (uint32_t v = 0; v < kVecs; ++v) {
+      const uint32_t wi = (v * kThreads + tid) * kWPV;
+      if (wi + kWPV <= tileN) {
+        const u32x4 val = *(lp<const u32x4>)&buf[wi];
+        st16((gp<void>)(y + t0 + wi), make_uint4(val.x, val.y, val.z, val.w));
+      } else {
+        for (uint32_t k = wi; k < tileN && k < wi + kWPV; ++k) y[t0 + k] = buf[k];
+      }
+    }
+  } else {
+    for (uint32_t i = tid; i < tileN; i += kThreads) y[t0 + i] = buf[i];
   }
 }
 
 template <int FT>
 void sparseCompressT(StackDeviceMemory& res, const FloatCompressConfig& config, uint32_t nb,
                      const BatchDesc& in, uint32_t maxN, const uint64_t* outPtrs_dev,
-                     const BatchDesc& denseOut, uint32_t* outSize_dev, hipStream_t s) {
+                     const BatchDesc& denseOut, uint32_t* outSize_dev, hipStream_t s, bool inAligned16) {
   const uint32_t tiles = std::max(1u, divUp(maxN, kTileWords));
-  auto tileCounts = res.alloc<uint32_t>(s, size_t(nb) * tiles);
   auto listLen = res.alloc<uint32_t>(s, nb);
+  auto poisoned = res.alloc<uint8_t>(s, nb);
   auto list = res.alloc<uint8_t>(s, size_t(nb) * (roundUp(maxN, 16) + 16) * sizeof(WordOf<FT>));
   std::vector<uint64_t> listPtrs(nb);
   for (uint32_t i = 0; i < nb; ++i) {
@@ -270,18 +313,22 @@ void sparseCompressT(StackDeviceMemory& res, const FloatCompressConfig& config, 
   }
   auto listPtrsDev = res.alloc<uint64_t>(s, nb);
   StackDeviceMemory::copyToDevice(listPtrsDev.data(), listPtrs.data(), nb * 8, s);
-  for (uint32_t y0 = 0; y0 < nb; y0 += kMaxGridY) {
-    const uint32_t ny = std::min(kMaxGridY, nb - y0);
-    {
+  {
+    // epoch-tagged look-back flags, one per (element, tile)
+    SyncLease lease(res, s, size_t(nb) * tiles * 8);
+    for (uint32_t y0 = 0; y0 < nb; y0 += kMaxGridY) {
+      const uint32_t ny = std::min(kMaxGridY, nb - y0);
       prof::Scope p("sparse", s);
-      k_sparseBitmap<FT><<<dim3(tiles, ny), kThreads, 0, s>>>(in, outPtrs_dev, y0, tiles,
-                                                               tileCounts.data());
-      HIP_LAUNCH_CHECK();
-      k_sparseScan<FT><<<ny, kThreads, 0, s>>>(in, y0, tiles, nullptr, tileCounts.data(),
-                                               listLen.data());
-      HIP_LAUNCH_CHECK();
-      k_sparseCompact<FT><<<dim3(tiles, ny), kThreads, 0, s>>>(in, y0, tiles, tileCounts.data(),
-                                                                listPtrsDev.data());
+      auto* f = reinterpret_cast<uint64_t*>(lease.base);
+      if (inAligned16) {
+        k_sparseCompress<FT, true><<<dim3(tiles, ny), kThreads, 0, s>>>(
+            in, outPtrs_dev, y0, tiles, listPtrsDev.data(), listLen.data(), f, lease.epoch, spinCap(),
+            poisoned.data(), deviceErrorWord());
+      } else {
+        k_sparseCompress<FT, false><<<dim3(tiles, ny), kThreads, 0, s>>>(
+            in, outPtrs_dev, y0, tiles, listPtrsDev.data(), listLen.data(), f, lease.epoch, spinCap(),
+            poisoned.data(), deviceErrorWord());
+      }
       HIP_LAUNCH_CHECK();
     }
   }
@@ -289,7 +336,7 @@ void sparseCompressT(StackDeviceMemory& res, const FloatCompressConfig& config, 
   floatCompressDescs(res, config, nb, BatchDesc::pointers(listPtrsDev.data(), listLen.data()),
                      maxN, denseOut, outSize_dev, s, nullptr, true);
   if (outSize_dev) {
-    k_sparseAddSizes<<<divUp(nb, 128), 128, 0, s>>>(in, nb, outSize_dev);
+    k_sparseAddSizes<<<divUp(nb, 128), 128, 0, s>>>(in, nb, poisoned.data(), outSize_dev);
     HIP_LAUNCH_CHECK();
   }
 }
@@ -299,11 +346,10 @@ FloatDecompressStatus sparseDecompressT(StackDeviceMemory& res,
                                         const FloatDecompressConfig& config, uint32_t nb,
                                         const BatchDesc& in, const BatchDesc& out,
                                         uint32_t maxCap, uint8_t* outSuccess_dev,
-                                        uint32_t* outSize_dev, hipStream_t s) {
+                                        uint32_t* outSize_dev, hipStream_t s, bool outAligned16) {
   const uint32_t tiles = std::max(1u, divUp(maxCap, kTileWords));
   auto densePtrs = res.alloc<uint64_t>(s, nb);
   auto sizes = res.alloc<uint32_t>(s, nb);
-  auto tileCounts = res.alloc<uint32_t>(s, size_t(nb) * tiles);
   auto denseOk = res.alloc<uint8_t>(s, nb);
   auto list = res.alloc<uint8_t>(s, size_t(nb) * (roundUp(maxCap, 16) + 16) * sizeof(WordOf<FT>));
   std::vector<uint64_t> listPtrs(nb);
@@ -313,14 +359,9 @@ FloatDecompressStatus sparseDecompressT(StackDeviceMemory& res,
   }
   auto listPtrsDev = res.alloc<uint64_t>(s, nb);
   StackDeviceMemory::copyToDevice(listPtrsDev.data(), listPtrs.data(), nb * 8, s);
-  for (uint32_t y0 = 0; y0 < nb; y0 += kMaxGridY) {
-    const uint32_t ny = std::min(kMaxGridY, nb - y0);
+  {
     prof::Scope p("sparse", s);
-    k_sparseHeaders<<<dim3(tiles, ny), kThreads, 0, s>>>(in, y0, tiles, densePtrs.data(),
-                                                          sizes.data(), tileCounts.data());
-    HIP_LAUNCH_CHECK();
-    k_sparseScan<FT><<<ny, kThreads, 0, s>>>(in, y0, tiles, sizes.data(), tileCounts.data(),
-                                             nullptr);
+    k_sparseHeaders<<<divUp(nb, 128), 128, 0, s>>>(in, nb, densePtrs.data(), sizes.data());
     HIP_LAUNCH_CHECK();
   }
   // dense decode of the nonzero list (capacity: the largest output)
@@ -342,12 +383,20 @@ FloatDecompressStatus sparseDecompressT(StackDeviceMemory& res,
                                        maxCap + 1, s);
     if (!status.errorInfo.empty()) status.error = FloatDecompressError::ChecksumMismatch;
   }
+  SyncLease lease(res, s, size_t(nb) * tiles * 8);
+  auto* f = reinterpret_cast<uint64_t*>(lease.base);
   for (uint32_t y0 = 0; y0 < nb; y0 += kMaxGridY) {
     const uint32_t ny = std::min(kMaxGridY, nb - y0);
     prof::Scope p("sparse", s);
-    k_sparseExpand<FT><<<dim3(tiles, ny), kThreads, 0, s>>>(
-        in, out, y0, tiles, sizes.data(), tileCounts.data(), listPtrsDev.data(), denseOk.data(),
-        outSuccess_dev, outSize_dev);
+    if (outAligned16) {
+      k_sparseExpand<FT, true><<<dim3(tiles, ny), kThreads, 0, s>>>(
+          in, out, y0, tiles, sizes.data(), listPtrsDev.data(), denseOk.data(), outSuccess_dev, outSize_dev, f,
+          lease.epoch, spinCap(), deviceErrorWord());
+    } else {
+      k_sparseExpand<FT, false><<<dim3(tiles, ny), kThreads, 0, s>>>(
+          in, out, y0, tiles, sizes.data(), listPtrsDev.data(), denseOk.data(), outSuccess_dev, outSize_dev, f,
+          lease.epoch, spinCap(), deviceErrorWord());
+    }
     HIP_LAUNCH_CHECK();
   }
   return status;
@@ -395,11 +444,13 @@ void floatCompressSparse(StackDeviceMemory& res, const FloatCompressConfig& conf
   const uint32_t* szD = reinterpret_cast<const uint32_t*>(dpD + numInBatch);
   auto inD = BatchDesc::pointers(ipD, szD);
   auto denseOut = BatchDesc::pointers(dpD, nullptr);
+  bool aligned = true;
+  for (uint32_t i = 0; i < numInBatch; ++i) aligned = aligned && ip[i] % 16 == 0;
   switch (ft) {
-    case 1: sparseCompressT<1>(res, config, numInBatch, inD, maxN, opD, denseOut, outSize_dev, stream); break;
-    case 2: sparseCompressT<2>(res, config, numInBatch, inD, maxN, opD, denseOut, outSize_dev, stream); break;
-    case 3: sparseCompressT<3>(res, config, numInBatch, inD, maxN, opD, denseOut, outSize_dev, stream); break;
-    default: sparseCompressT<4>(res, config, numInBatch, inD, maxN, opD, denseOut, outSize_dev, stream); break;
+    case 1: sparseCompressT<1>(res, config, numInBatch, inD, maxN, opD, denseOut, outSize_dev, stream, aligned); break;
+    case 2: sparseCompressT<2>(res, config, numInBatch, inD, maxN, opD, denseOut, outSize_dev, stream, aligned); break;
+    case 3: sparseCompressT<3>(res, config, numInBatch, inD, maxN, opD, denseOut, outSize_dev, stream, aligned); break;
+    default: sparseCompressT<4>(res, config, numInBatch, inD, maxN, opD, denseOut, outSize_dev, stream, aligned); break;
   }
 }
 
@@ -431,11 +482,13 @@ FloatDecompressStatus floatDecompressSparse(StackDeviceMemory& res,
   const uint32_t* capD = reinterpret_cast<const uint32_t*>(opD + numInBatch);
   auto inD = BatchDesc::pointers(ipD, nullptr);
   auto outD = BatchDesc::pointers(opD, capD);
+  bool aligned = true;
+  for (uint32_t i = 0; i < numInBatch; ++i) aligned = aligned && ptrs[numInBatch + i] % 16 == 0;
   switch (ft) {
-    case 1: return sparseDecompressT<1>(res, config, numInBatch, inD, outD, maxCap, outSuccess_dev, outSize_dev, stream);
-    case 2: return sparseDecompressT<2>(res, config, numInBatch, inD, outD, maxCap, outSuccess_dev, outSize_dev, stream);
-    case 3: return sparseDecompressT<3>(res, config, numInBatch, inD, outD, maxCap, outSuccess_dev, outSize_dev, stream);
-    default: return sparseDecompressT<4>(res, config, numInBatch, inD, outD, maxCap, outSuccess_dev, outSize_dev, stream);
+    case 1: return sparseDecompressT<1>(res, config, numInBatch, inD, outD, maxCap, outSuccess_dev, outSize_dev, stream, aligned);
+    case 2: return sparseDecompressT<2>(res, config, numInBatch, inD, outD, maxCap, outSuccess_dev, outSize_dev, stream, aligned);
+    case 3: return sparseDecompressT<3>(res, config, numInBatch, inD, outD, maxCap, outSuccess_dev, outSize_dev, stream, aligned);
+    default: return sparseDecompressT<4>(res, config, numInBatch, inD, outD, maxCap, outSuccess_dev, outSize_dev, stream, aligned);
   }
 }
 
