@@ -5,10 +5,13 @@
 // float/GpuSparseFloatDecompress.{cu,cuh}.  The reference scans with one
 // thrust::exclusive_scan per batch element on the legacy default stream
 // between two cudaDeviceSynchronize calls (GpuSparseFloatCompress.cuh:360-369);
-// here compression is ONE pass over the input (k_sparseCompress: bitmap, tile
-// counts, decoupled look-back over the tiles of an element, compaction), and
-// decompression scans the bitmap's tile popcounts, fully stream-ordered (no
-// host or device-wide sync).
+// here both directions are reduce-then-scan over 4096-word tiles, fully
+// stream-ordered (no host or device-wide sync): compression reads the input
+// ONCE (k_sparseCount: bitmap, tile counts, nonzeros compacted within the
+// tile into a staging area; k_sparseScan: tile offsets; k_sparseGather: the
+// staged nonzeros to their list positions), decompression scans the bitmap's
+// tile popcounts and expands.  (A decoupled look-back across the tiles of
+// one element measured slower: with thousands of tiles its chain dominates.)
 //
 // Wire format: 16 B header {u32 N, 12 B zero}, bitmap
 // ceil(N/8) bytes (bit 7 of byte k <-> element 8k) padded to 16, then a dense
@@ -24,9 +27,7 @@
 #include "dietgpu/GpuFloatCodec.h"
 #include "decode.h"
 #include "encode.h"
-#include "lookback.h"
 #include "profile.h"
-#include "sync_arena.h"
 
 namespace dietgpu {
 
@@ -48,44 +49,14 @@ __device__ __forceinline__ bool isNonzero(WordOf<FT> w) {
   return w != 0;  // bitwise: -0.0 is "nonzero" (generate_bitmap :56)
 }
 
-// Compression in one pass.  grid (tiles, batch); a workgroup takes one
-// 4096-word tile of one element: it loads the tile (16 B vectors when the
-// element is 16 B aligned, coalesced) into LDS, then each wave takes 1024
-// consecutive words as 16 steps of 64 lanes: the ballot of nonzero flags is
-// the step's 64 bitmap bits (generate_bitmap :40-71) and its nonzeros'
-// ranks (v_mbcnt).  The tile's nonzero count goes through a decoupled
-// look-back over the element's earlier tiles (epoch-tagged flags, lookback.h);
-// then the nonzeros are scattered into the compacted list (fill_comp_input
-// :119-185, n-2 quirk included).  A look-back that runs out of polls marks the
-// element (its final outSize becomes 0) instead of guessing.
-template <int FT, bool kVec>
-__global__ __launch_bounds__(kThreads) void k_sparseCompress(BatchDesc in, const uint64_t* outPtrs,
-                                                             uint32_t batchOffset, uint32_t tilesPerElem,
-                                                             const uint64_t* __restrict__ listPtrs,
-                                                             uint32_t* __restrict__ listLen,
-                                                             uint64_t* __restrict__ flags, uint32_t epoch,
-                                                             uint32_t spinCap, uint8_t* __restrict__ poisoned,
-                                                             uint32_t* __restrict__ err) {
-  using W = WordOf<FT>;
-  constexpr uint32_t kSteps = kTileWords / kWaves / 64;
-  constexpr uint32_t kVecs = kTileWords * sizeof(W) / 16 / kThreads;  // 16 B vectors per thread
-  __shared__ __attribute__((aligned(16))) W buf[kTileWords];
-  __shared__ uint32_t waveCnt[kWaves];
-  __shared__ uint32_t exclS;
-  __shared__ uint32_t poisonS;
-  const uint32_t b = batchOffset + blockIdx.y;
-  const uint32_t n = in.size(b);
-  const uint32_t tile = blockIdx.x;
-  if (tile * kTileWords >= n && !(n == 0 && tile == 0)) return;
-  const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  gp<const W> x = (gp<const W>)in.start(b);
-  gp<uint8_t> o = (gp<uint8_t>)outPtrs[b];
-  if (tile == 0 && tid == 0) st16(o, make_uint4(n, 0, 0, 0));
-  const uint32_t t0 = tile * kTileWords;
-  const uint32_t tileN = min(kTileWords, n - min(n, t0));
-  // tile -> LDS (words past the element read as 0)
+// Load tile `tile` of an element (words past n read as 0) into LDS: 16 B
+// vectors when the element is 16 B aligned (coalesced), else words.
+template <typename W, bool kVec>
+__device__ __forceinline__ void loadTile(gp<const W> x, uint32_t t0, uint32_t tileN, W* buf) {
+  const uint32_t tid = threadIdx.x;
   if (kVec) {
     constexpr uint32_t kWPV = 16 / sizeof(W);
+    constexpr uint32_t kVecs = kTileWords * sizeof(W) / 16 / kThreads;
 #pragma unroll
     for (uint32_t v = 0; v < kVecs; ++v) {
       const uint32_t wi = (v * kThreads + tid) * kWPV;  // first word of the vector
@@ -104,15 +75,47 @@ __global__ __launch_bounds__(kThreads) void k_sparseCompress(BatchDesc in, const
 #pragma unroll 4
     for (uint32_t i = tid; i < kTileWords; i += kThreads) buf[i] = i < tileN ? x[t0 + i] : W(0);
   }
+}
+
+// s1: bitmap + tile count + tile-local compaction.  grid (tiles, batch); a
+// workgroup takes one 4096-word tile of one element into LDS, then each wave
+// takes 1024 consecutive words as 16 steps of 64 lanes: the ballot of nonzero
+// flags is the step's 64 bitmap bits (generate_bitmap :40-71) and its
+// nonzeros' ranks (v_mbcnt).  The nonzeros go, in order, to the tile's slice
+// of a staging area; the n-2 quirk (fill_comp_input :162-184) is one extra
+// staged slot: when x[n-2] == 0, a 0 precedes x[n-1]'s slot.
+template <int FT, bool kVec>
+__global__ __launch_bounds__(kThreads) void k_sparseCount(BatchDesc in, const uint64_t* outPtrs,
+                                                          uint32_t batchOffset, uint32_t tilesPerElem,
+                                                          uint32_t* __restrict__ tileCounts,
+                                                          WordOf<FT>* __restrict__ staging) {
+  using W = WordOf<FT>;
+  constexpr uint32_t kSteps = kTileWords / kWaves / 64;
+  __shared__ __attribute__((aligned(16))) W buf[kTileWords];
+  __shared__ uint32_t waveCnt[kWaves];
+  const uint32_t b = batchOffset + blockIdx.y;
+  const uint32_t n = in.size(b);
+  const uint32_t tile = blockIdx.x;
+  const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  gp<uint8_t> o = (gp<uint8_t>)outPtrs[b];
+  if (tile == 0 && tid == 0) st16(o, make_uint4(n, 0, 0, 0));
+  const uint32_t t0 = tile * kTileWords;
+  if (t0 >= n) {
+    if (tid == 0) tileCounts[uint64_t(b) * tilesPerElem + tile] = 0;
+    return;
+  }
+  gp<const W> x = (gp<const W>)in.start(b);
+  loadTile<W, kVec>(x, t0, min(kTileWords, n - t0), buf);
   __syncthreads();
-  // bitmap bits and counts, wave w: words [w * 1024, (w + 1) * 1024) of the tile
   const uint32_t bmBytes = (n + 7) / 8, bmPad = roundUp(bmBytes, 16);
+  // bitwise: -0.0 is "nonzero" (generate_bitmap :56)
+  const bool gap = n >= 2 && x[n - 2] == W(0);
   uint64_t m[kSteps];
   uint32_t cnt = 0;
 #pragma unroll
   for (uint32_t j = 0; j < kSteps; ++j) {
     const uint32_t q = w * (kTileWords / kWaves) + 64 * j;  // step's first word in the tile
-    m[j] = ballot(buf[q + lane] != W(0));  // bitwise: -0.0 is "nonzero" (generate_bitmap :56)
+    m[j] = ballot(buf[q + lane] != W(0));
     cnt += uint32_t(__popcll(m[j]));
     const uint32_t i0 = t0 + q;
     if (lane == 0 && i0 < n) {
@@ -121,120 +124,138 @@ __global__ __launch_bounds__(kThreads) void k_sparseCompress(BatchDesc in, const
       // zero the 16-byte padding after the last bitmap word
       const uint32_t end = i0 / 8 + 8;
       if (i0 + 64 >= n && end < bmPad) dst[1] = 0;
+      if (gap && i0 <= n - 1 && n - 1 < i0 + 64) cnt += 1;  // the extra slot
     }
   }
   if (lane == 0) waveCnt[w] = cnt;
   __syncthreads();
-  if (w == 0) {
-    const uint32_t total = waveCnt[0] + waveCnt[1] + waveCnt[2] + waveCnt[3];
-    bool pz = false;
-    const uint32_t excl =
-        lookBackPoison(G(flags) + uint64_t(b) * tilesPerElem, tile, total, epoch, spinCap, pz);
-    if (lane == 0) {
-      exclS = excl;
-      poisonS = pz ? 1u : 0u;
-      if ((tile + 1) * kTileWords >= n) {  // the element's last tile
-        uint32_t len = 0;
-        if (n == 1) {
-          len = buf[0] != W(0) ? 1u : 0u;
-        } else if (n >= 2) {
-          // idx[n-2] + flag[n-1] + 1 == nnz - flag[n-2] + 1
-          len = excl + total - (x[n - 2] != W(0) ? 1u : 0u) + 1u;
-        }
-        listLen[b] = pz ? 0u : len;
-        poisoned[b] = pz ? 1 : 0;
-        if (pz) __hip_atomic_fetch_add(G(err), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-  }
-  __syncthreads();
-  if (poisonS) return;
-  uint32_t pos = exclS;
+  uint32_t pos = 0;
   for (uint32_t k = 0; k < w; ++k) pos += waveCnt[k];
-  gp<W> list = (gp<W>)listPtrs[b];
-  // the n-2 quirk: x[n-1] goes to idx[n-2] + 1 and, when x[n-2] == 0, the
-  // skipped slot idx[n-2] is part of the list (written as 0)
-  const bool gap = n >= 2 && x[n - 2] == W(0);
+  if (tid == 0) tileCounts[uint64_t(b) * tilesPerElem + tile] = waveCnt[0] + waveCnt[1] + waveCnt[2] + waveCnt[3];
+  W* st = staging + (uint64_t(b) * tilesPerElem + tile) * (kTileWords + 1);
 #pragma unroll
   for (uint32_t j = 0; j < kSteps; ++j) {
-    const uint32_t q = w * (kTileWords / kWaves) + 64 * j + lane;
-    const uint32_t i = t0 + q;
-    const W v = buf[q];
+    const uint32_t q = w * (kTileWords / kWaves) + 64 * j;
+    const uint32_t i = t0 + q + lane;
+    const W v = buf[q + lane];
     const uint32_t dst = pos + mbcnt(m[j]);
     if (i + 1 == n && gap) {
-      list[dst] = W(0);
-      if (v != W(0)) list[dst + 1] = v;
+      st[dst] = W(0);
+      if (v != W(0)) st[dst + 1] = v;
     } else if (v != W(0)) {
-      list[dst] = v;
+      st[dst] = v;
     }
-    pos += uint32_t(__popcll(m[j]));
+    pos += uint32_t(__popcll(m[j])) + ((gap && t0 + q <= n - 1 && n - 1 < t0 + q + 64) ? 1u : 0u);
   }
 }
 
-// outSize of the sparse archive: header + padded bitmap + dense archive; 0 for
-// an element whose compaction was abandoned (k_sparseCompress)
-__global__ void k_sparseAddSizes(BatchDesc in, uint32_t numInBatch, const uint8_t* __restrict__ poisoned,
-                                 uint32_t* __restrict__ outSize) {
-  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b < numInBatch && outSize)
-    outSize[b] = poisoned[b] ? 0u : outSize[b] + 16 + roundUp((in.size(b) + 7) / 8, 16);
+// s2 / d2: exclusive scan of tile counts per element (in place); optional
+// total (the compacted list's length).  grid (batch)
+__global__ __launch_bounds__(kThreads) void k_sparseScan(uint32_t batchOffset, uint32_t tilesPerElem,
+                                                         const uint32_t* __restrict__ sizes, BatchDesc in,
+                                                         uint32_t* __restrict__ tileCounts,
+                                                         uint32_t* __restrict__ total) {
+  __shared__ uint32_t red[kWaves];
+  const uint32_t b = batchOffset + blockIdx.x;
+  const uint32_t n = sizes ? sizes[b] : in.size(b);
+  const uint32_t tiles = min(divUp(n, kTileWords), tilesPerElem);
+  uint32_t* tc = tileCounts + uint64_t(b) * tilesPerElem;
+  uint32_t carry = 0;
+  for (uint32_t t0 = 0; t0 < tiles; t0 += kThreads) {
+    const uint32_t t = t0 + threadIdx.x;
+    const uint32_t v = t < tiles ? tc[t] : 0u;
+    uint32_t all = 0;
+    const uint32_t ex = blockExclusiveScan<kThreads>(v, red, &all);
+    if (t < tiles) tc[t] = carry + ex;
+    carry += all;
+    __syncthreads();
+  }
+  if (total && threadIdx.x == 0) total[b] = carry;
 }
 
-// d1: headers -> dense-archive pointers and sizes.  One thread per element.
-__global__ void k_sparseHeaders(BatchDesc in, uint32_t numInBatch, uint64_t* __restrict__ densePtrs,
-                                uint32_t* __restrict__ sizes) {
+// s3: staged nonzeros -> their list positions.  grid (tiles, batch)
+template <int FT>
+__global__ __launch_bounds__(kThreads) void k_sparseGather(BatchDesc in, uint32_t batchOffset,
+                                                           uint32_t tilesPerElem,
+                                                           const uint32_t* __restrict__ tileOff,
+                                                           const uint32_t* __restrict__ listLen,
+                                                           const WordOf<FT>* __restrict__ staging,
+                                                           const uint64_t* __restrict__ listPtrs) {
+  using W = WordOf<FT>;
+  const uint32_t b = batchOffset + blockIdx.y;
+  const uint32_t n = in.size(b);
+  const uint32_t tile = blockIdx.x;
+  if (tile * kTileWords >= n) return;
+  const uint64_t row = uint64_t(b) * tilesPerElem + tile;
+  const uint32_t off = tileOff[row];
+  const bool lastTile = (tile + 1) * kTileWords >= n;
+  const uint32_t cnt = (lastTile ? listLen[b] : tileOff[row + 1]) - off;
+  const W* st = staging + row * (kTileWords + 1);
+  gp<W> list = (gp<W>)listPtrs[b];
+  for (uint32_t i = threadIdx.x; i < cnt; i += kThreads) list[off + i] = st[i];
+}
+
+// outSize of the sparse archive: header + padded bitmap + dense archive
+__global__ void k_sparseAddSizes(BatchDesc in, uint32_t numInBatch, uint32_t* __restrict__ outSize) {
   const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= numInBatch) return;
-  const uint8_t* a = in.start(b);
-  const uint32_t n = reinterpret_cast<const uint32_t*>(a)[0];
-  densePtrs[b] = reinterpret_cast<uint64_t>(a + 16 + roundUp((n + 7) / 8, 16));
-  sizes[b] = n;
+  if (b < numInBatch && outSize) outSize[b] += 16 + roundUp((in.size(b) + 7) / 8, 16);
+}
+
+// d1: headers -> dense-archive pointers and sizes, and per-tile popcounts of
+// the bitmap.  grid (tiles, batch)
+__global__ __launch_bounds__(kThreads) void k_sparseHeaders(BatchDesc in, uint32_t batchOffset,
+                                                            uint32_t tilesPerElem,
+                                                            uint64_t* __restrict__ densePtrs,
+                                                            uint32_t* __restrict__ sizes,
+                                                            uint32_t* __restrict__ tileCounts) {
+  __shared__ uint32_t red[kWaves];
+  const uint32_t b = batchOffset + blockIdx.y;
+  gp<const uint8_t> a = (gp<const uint8_t>)in.start(b);
+  const uint32_t n = ((gp<const uint32_t>)a)[0];
+  const uint32_t tile = blockIdx.x;
+  if (tile == 0 && threadIdx.x == 0) {
+    densePtrs[b] = reinterpret_cast<uint64_t>(in.start(b) + 16 + roundUp((n + 7) / 8, 16));
+    sizes[b] = n;
+  }
+  if (tile >= tilesPerElem) return;
+  // 512 bitmap bytes per tile: 2 bytes per thread
+  const uint32_t bytes0 = tile * (kTileWords / 8), bmBytes = (n + 7) / 8;
+  uint32_t c = 0;
+  for (uint32_t k = threadIdx.x; k < kTileWords / 8; k += kThreads)
+    if (bytes0 + k < bmBytes) c += __popc(a[16 + bytes0 + k]);
+  c = blockSum<kThreads>(c, red);
+  if (threadIdx.x == 0) tileCounts[uint64_t(b) * tilesPerElem + tile] = c;
 }
 
 // d3: expand the decoded nonzero list into the output (fill_in_nonzeros
-// :95-144).  grid (tiles, batch); per 4096-word tile: the bitmap's popcount,
-// a decoupled look-back over the element's earlier tiles for the tile's
-// first list index, the expansion into LDS, and 16 B stores when the output
-// is 16 B aligned.  The element's last tile reports success and size (a
-// look-back that runs out of polls reports failure).
+// :95-144).  grid (tiles, batch); per 4096-word tile: expansion into LDS from
+// the tile's first list index, then 16 B stores when the output is 16 B
+// aligned.
 template <int FT, bool kVec>
 __global__ __launch_bounds__(kThreads) void k_sparseExpand(BatchDesc in, BatchDesc out, uint32_t batchOffset,
                                                            uint32_t tilesPerElem, const uint32_t* __restrict__ sizes,
+                                                           const uint32_t* __restrict__ tileOff,
                                                            const uint64_t* __restrict__ listPtrs,
                                                            const uint8_t* __restrict__ denseOk,
                                                            uint8_t* __restrict__ outSuccess,
-                                                           uint32_t* __restrict__ outSize, uint64_t* __restrict__ flags,
-                                                           uint32_t epoch, uint32_t spinCap,
-                                                           uint32_t* __restrict__ err) {
+                                                           uint32_t* __restrict__ outSize) {
   using W = WordOf<FT>;
   constexpr uint32_t kSteps = kTileWords / kWaves / 64;
   constexpr uint32_t kVecs = kTileWords * sizeof(W) / 16 / kThreads;
   __shared__ __attribute__((aligned(16))) W buf[kTileWords];
   __shared__ uint32_t waveCnt[kWaves];
-  __shared__ uint32_t exclS, poisonS;
   const uint32_t b = batchOffset + blockIdx.y;
   const uint32_t n = sizes[b];
   const bool ok = denseOk[b] != 0 && out.size(b) >= n;
   const uint32_t tile = blockIdx.x;
   const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  if (n == 0) {
-    if (tile == 0 && tid == 0) {
-      if (outSuccess) outSuccess[b] = ok ? 1 : 0;
-      if (outSize) outSize[b] = 0;
-    }
-    return;
+  if (tile == 0 && tid == 0) {
+    if (outSuccess) outSuccess[b] = ok ? 1 : 0;
+    if (outSize) outSize[b] = n;  // fill_in_nonzeros :107-109
   }
-  if (tile * kTileWords >= n) return;
-  const bool last = (tile + 1) * kTileWords >= n;
-  if (!ok) {
-    if (last && tid == 0) {
-      if (outSuccess) outSuccess[b] = 0;
-      if (outSize) outSize[b] = n;  // fill_in_nonzeros :107-109
-    }
-    return;
-  }
-  gp<const uint8_t> bm = (gp<const uint8_t>)in.start(b) + 16;
   const uint32_t t0 = tile * kTileWords;
+  if (!ok || t0 >= n) return;
+  gp<const uint8_t> bm = (gp<const uint8_t>)in.start(b) + 16;
   uint64_t m[kSteps];
   uint32_t cnt = 0;
 #pragma unroll
@@ -246,24 +267,7 @@ __global__ __launch_bounds__(kThreads) void k_sparseExpand(BatchDesc in, BatchDe
   }
   if (lane == 0) waveCnt[w] = cnt;
   __syncthreads();
-  if (w == 0) {
-    bool pz = false;
-    const uint32_t total = waveCnt[0] + waveCnt[1] + waveCnt[2] + waveCnt[3];
-    const uint32_t excl =
-        lookBackPoison(G(flags) + uint64_t(b) * tilesPerElem, tile, total, epoch, spinCap, pz);
-    if (lane == 0) {
-      exclS = excl;
-      poisonS = pz ? 1u : 0u;
-      if (last) {
-        if (outSuccess) outSuccess[b] = pz ? 0 : 1;
-        if (outSize) outSize[b] = n;
-        if (pz) __hip_atomic_fetch_add(G(err), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-  }
-  __syncthreads();
-  if (poisonS) return;
-  uint32_t pos = exclS;
+  uint32_t pos = tileOff[uint64_t(b) * tilesPerElem + tile];
   for (uint32_t k = 0; k < w; ++k) pos += waveCnt[k];
   gp<const W> list = (gp<const W>)listPtrs[b];
   // x[n-1] is read from idx[n-2] + 1 (fill_in_nonzeros :139-144)
@@ -303,8 +307,10 @@ void sparseCompressT(StackDeviceMemory& res, const FloatCompressConfig& config, 
                      const BatchDesc& in, uint32_t maxN, const uint64_t* outPtrs_dev,
                      const BatchDesc& denseOut, uint32_t* outSize_dev, hipStream_t s, bool inAligned16) {
   const uint32_t tiles = std::max(1u, divUp(maxN, kTileWords));
+  auto tileCounts = res.alloc<uint32_t>(s, size_t(nb) * tiles);
   auto listLen = res.alloc<uint32_t>(s, nb);
-  auto poisoned = res.alloc<uint8_t>(s, nb);
+  // per tile: its nonzeros in order, plus the n-2 quirk's slot
+  auto staging = res.alloc<WordOf<FT>>(s, size_t(nb) * tiles * (kTileWords + 1));
   auto list = res.alloc<uint8_t>(s, size_t(nb) * (roundUp(maxN, 16) + 16) * sizeof(WordOf<FT>));
   std::vector<uint64_t> listPtrs(nb);
   for (uint32_t i = 0; i < nb; ++i) {
@@ -313,30 +319,28 @@ void sparseCompressT(StackDeviceMemory& res, const FloatCompressConfig& config, 
   }
   auto listPtrsDev = res.alloc<uint64_t>(s, nb);
   StackDeviceMemory::copyToDevice(listPtrsDev.data(), listPtrs.data(), nb * 8, s);
-  {
-    // epoch-tagged look-back flags, one per (element, tile)
-    SyncLease lease(res, s, size_t(nb) * tiles * 8);
-    for (uint32_t y0 = 0; y0 < nb; y0 += kMaxGridY) {
-      const uint32_t ny = std::min(kMaxGridY, nb - y0);
-      prof::Scope p("sparse", s);
-      auto* f = reinterpret_cast<uint64_t*>(lease.base);
-      if (inAligned16) {
-        k_sparseCompress<FT, true><<<dim3(tiles, ny), kThreads, 0, s>>>(
-            in, outPtrs_dev, y0, tiles, listPtrsDev.data(), listLen.data(), f, lease.epoch, spinCap(),
-            poisoned.data(), deviceErrorWord());
-      } else {
-        k_sparseCompress<FT, false><<<dim3(tiles, ny), kThreads, 0, s>>>(
-            in, outPtrs_dev, y0, tiles, listPtrsDev.data(), listLen.data(), f, lease.epoch, spinCap(),
-            poisoned.data(), deviceErrorWord());
-      }
-      HIP_LAUNCH_CHECK();
+  for (uint32_t y0 = 0; y0 < nb; y0 += kMaxGridY) {
+    const uint32_t ny = std::min(kMaxGridY, nb - y0);
+    prof::Scope p("sparse", s);
+    if (inAligned16) {
+      k_sparseCount<FT, true><<<dim3(tiles, ny), kThreads, 0, s>>>(in, outPtrs_dev, y0, tiles, tileCounts.data(),
+                                                                    staging.data());
+    } else {
+      k_sparseCount<FT, false><<<dim3(tiles, ny), kThreads, 0, s>>>(in, outPtrs_dev, y0, tiles, tileCounts.data(),
+                                                                     staging.data());
     }
+    HIP_LAUNCH_CHECK();
+    k_sparseScan<<<ny, kThreads, 0, s>>>(y0, tiles, nullptr, in, tileCounts.data(), listLen.data());
+    HIP_LAUNCH_CHECK();
+    k_sparseGather<FT><<<dim3(tiles, ny), kThreads, 0, s>>>(in, y0, tiles, tileCounts.data(), listLen.data(),
+                                                             staging.data(), listPtrsDev.data());
+    HIP_LAUNCH_CHECK();
   }
   // (the compacted lists are 16 B-aligned slices of one arena allocation)
   floatCompressDescs(res, config, nb, BatchDesc::pointers(listPtrsDev.data(), listLen.data()),
                      maxN, denseOut, outSize_dev, s, nullptr, true);
   if (outSize_dev) {
-    k_sparseAddSizes<<<divUp(nb, 128), 128, 0, s>>>(in, nb, poisoned.data(), outSize_dev);
+    k_sparseAddSizes<<<divUp(nb, 128), 128, 0, s>>>(in, nb, outSize_dev);
     HIP_LAUNCH_CHECK();
   }
 }
@@ -359,9 +363,14 @@ FloatDecompressStatus sparseDecompressT(StackDeviceMemory& res,
   }
   auto listPtrsDev = res.alloc<uint64_t>(s, nb);
   StackDeviceMemory::copyToDevice(listPtrsDev.data(), listPtrs.data(), nb * 8, s);
-  {
+  auto tileCounts = res.alloc<uint32_t>(s, size_t(nb) * tiles);
+  for (uint32_t y0 = 0; y0 < nb; y0 += kMaxGridY) {
+    const uint32_t ny = std::min(kMaxGridY, nb - y0);
     prof::Scope p("sparse", s);
-    k_sparseHeaders<<<divUp(nb, 128), 128, 0, s>>>(in, nb, densePtrs.data(), sizes.data());
+    k_sparseHeaders<<<dim3(tiles, ny), kThreads, 0, s>>>(in, y0, tiles, densePtrs.data(), sizes.data(),
+                                                          tileCounts.data());
+    HIP_LAUNCH_CHECK();
+    k_sparseScan<<<ny, kThreads, 0, s>>>(y0, tiles, sizes.data(), in, tileCounts.data(), nullptr);
     HIP_LAUNCH_CHECK();
   }
   // dense decode of the nonzero list (capacity: the largest output)
@@ -383,19 +392,17 @@ FloatDecompressStatus sparseDecompressT(StackDeviceMemory& res,
                                        maxCap + 1, s);
     if (!status.errorInfo.empty()) status.error = FloatDecompressError::ChecksumMismatch;
   }
-  SyncLease lease(res, s, size_t(nb) * tiles * 8);
-  auto* f = reinterpret_cast<uint64_t*>(lease.base);
   for (uint32_t y0 = 0; y0 < nb; y0 += kMaxGridY) {
     const uint32_t ny = std::min(kMaxGridY, nb - y0);
     prof::Scope p("sparse", s);
     if (outAligned16) {
       k_sparseExpand<FT, true><<<dim3(tiles, ny), kThreads, 0, s>>>(
-          in, out, y0, tiles, sizes.data(), listPtrsDev.data(), denseOk.data(), outSuccess_dev, outSize_dev, f,
-          lease.epoch, spinCap(), deviceErrorWord());
+          in, out, y0, tiles, sizes.data(), tileCounts.data(), listPtrsDev.data(), denseOk.data(), outSuccess_dev,
+          outSize_dev);
     } else {
       k_sparseExpand<FT, false><<<dim3(tiles, ny), kThreads, 0, s>>>(
-          in, out, y0, tiles, sizes.data(), listPtrsDev.data(), denseOk.data(), outSuccess_dev, outSize_dev, f,
-          lease.epoch, spinCap(), deviceErrorWord());
+          in, out, y0, tiles, sizes.data(), tileCounts.data(), listPtrsDev.data(), denseOk.data(), outSuccess_dev,
+          outSize_dev);
     }
     HIP_LAUNCH_CHECK();
   }
