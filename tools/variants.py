@@ -1,0 +1,109 @@
+"""Dev tool: build kernel-variant libraries for same-box A/B timing.
+
+Each variant is a scratch copy of dietgpu_fork_amd/csrc (under /tmp/var,
+never the product tree) with a few source substitutions, built into
+tools/ablibs/<name>.so (git-ignored); tools/ab.sh (c2 bench),
+tools/debug/extras_ab.sh (secondary configs) and tools/debug/sp_ab.sh
+(sparse) swap them in on the GPU box.  The variants below are the round-2
+experiments recorded in DESIGN.md section 7; a substitution that no longer
+matches the current sources fails loudly.
+    usage: python tools/variants.py name..."""
+import os, shutil, subprocess, sys
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+P = "pcompress.h"
+NOENC = (P, "const bool encOn = hasE && uwE0 != 0 && !poisonE;", "const bool encOn = false;")
+NOHIST = [(P, "__hip_atomic_fetch_add(hcol + __umul24(sym, pc::kHistStride), 1u,", "if (sym == 0x1234u) __hip_atomic_fetch_add(hcol + __umul24(sym, pc::kHistStride), 1u,"),
+          (P, "__hip_atomic_fetch_add(hcol + __umul24(sym, pc::kHistStride), add,", "if (sym == 0x1234u) __hip_atomic_fetch_add(hcol + __umul24(sym, pc::kHistStride), add,")]
+NOSPLITST = (P, "splitVec<FT>(v, i0, it.n, raw, myT + off, myT + off, store);", "splitVec<FT>(v, i0, it.n, raw, myT + off, myT + off, false);")
+NONORM = [(P, "bool ok = it.team == 1;", "bool ok = true;"),
+          (P, "for (uint32_t k0 = 0; k0 < it.team; k0 += 16) {", "for (uint32_t k0 = 0; k0 < 0; k0 += 16) {"),
+          (P, "const uint32_t q = it.n == 0 ? 0u : normalizeCount(count, it.n, A().pb, keys, red);", "const uint32_t q = tid == 0 ? 1024u : 0u;")]
+STAMP = [
+    (P, "namespace pc {", "__device__ unsigned long long g_stamp[4096 * 8 * 6];\n#define STAMP(ph) do { if (tid == 0 && itc < 8) { unsigned long long t_ = __builtin_amdgcn_s_memrealtime(); asm volatile(\"\" : \"+v\"(t_)); ((volatile unsigned long long*)g_stamp)[(blockIdx.x * 8 + itc) * 6 + (ph)] = t_; } } while (0)\nnamespace pc {"),
+    (P, "    if (!hasE && !hasL) break;\n", "    if (!hasE && !hasL) break;\n    STAMP(0);\n"),
+    (P, "    if (hasL) publish(itemOf(iL, A(), IN()));", "    STAMP(1);\n    if (hasL) publish(itemOf(iL, A(), IN()));"),
+    (P, "    if (hasE) place(itemOf(iE, A(), IN()), poisonE, ckE);", "    STAMP(2);\n    if (hasE) place(itemOf(iE, A(), IN()), poisonE, ckE);\n    STAMP(3);"),
+    (P, "      iN = itemAt(++round);", "      STAMP(4);\n      iN = itemAt(++round);"),
+    (P, "    iE = iL;\n    iL = iN;", "    STAMP(5);\n    ++itc;\n    iE = iL;\n    iL = iN;"),
+    (P, "  uint32_t ckE = 0;\n", "  uint32_t ckE = 0;\n  uint32_t itc = 0;\n"),
+    ("codec.hip", "uint32_t deviceErrorCount(bool reset) {", "extern \"C\" void* dietgpu_debug_stamps() { void* p = nullptr; (void)hipGetSymbolAddress(&p, HIP_SYMBOL(g_stamp)); return p; }\n\nuint32_t deviceErrorCount(bool reset) {"),
+]
+STAMP2 = [
+    (P, "namespace pc {", "__device__ unsigned long long g_stamp[4096 * 8 * 16];\n#define STAMP(ph) do { if (tid == 0 && itc < 8) { unsigned long long t_ = __builtin_amdgcn_s_memrealtime(); asm volatile(\"\" : \"+v\"(t_)); ((volatile unsigned long long*)g_stamp)[(blockIdx.x * 8 + itc) * 16 + (ph)] = t_; } } while (0)\nnamespace pc {"),
+    (P, "    if (!hasE && !hasL) break;\n", "    if (!hasE && !hasL) break;\n    STAMP(0);\n"),
+    (P, "    if (hasL) publish(itemOf(iL, A(), IN()));", "    STAMP(1);\n    if (hasL) publish(itemOf(iL, A(), IN()));"),
+    (P, "    if (hasE) place(itemOf(iE, A(), IN()), poisonE, ckE);", "    STAMP(2);\n    if (hasE) place(itemOf(iE, A(), IN()), poisonE, ckE);\n    STAMP(3);"),
+    (P, "      iN = itemAt(++round);", "      STAMP(4);\n      iN = itemAt(++round);"),
+    (P, "    iE = iL;\n    iL = iN;", "    STAMP(5);\n    ++itc;\n    iE = iL;\n    iL = iN;"),
+    (P, "  uint32_t ck = 0;\n", "  uint32_t ck = 0;\n  uint32_t itc = 0;\n"),
+    # inside place
+    (P, "    if (p.flushed[0] | p.flushed[1]) asm volatile(\"s_waitcnt vmcnt(0)\" ::: \"memory\");\n    __syncthreads();\n", "    if (p.flushed[0] | p.flushed[1]) asm volatile(\"s_waitcnt vmcnt(0)\" ::: \"memory\");\n    __syncthreads();\n    STAMP(6);\n"),
+    (P, "    if (it.x == 0) {\n      // header fields known before encoding", "    STAMP(7);\n    if (it.x == 0) {\n      // header fields known before encoding"),
+    (P, "    if (nk == 0) return;\n    // payload", "    STAMP(8);\n    if (nk == 0) return;\n    // payload"),
+    # inside barrierNormalize
+    (P, "    const bool timedOut = readfirst(stateS) != 0;\n", "    const bool timedOut = readfirst(stateS) != 0;\n    STAMP(9);\n"),
+    (P, "    const uint32_t q = it.n == 0 ? 0u : normalizeCount(count, it.n, A().pb, keys, red);", "    STAMP(10);\n    const uint32_t q = it.n == 0 ? 0u : normalizeCount(count, it.n, A().pb, keys, red);\n    STAMP(11);"),
+    # inside publish: after the vmcnt(0)
+    (P, "    asm volatile(\"s_waitcnt vmcnt(0)\" ::: \"memory\");\n    __syncthreads();\n    if (tid == 0) stSc1(G(A().arrive) + it.i, A().epoch);", "    STAMP(12);\n    asm volatile(\"s_waitcnt vmcnt(0)\" ::: \"memory\");\n    __syncthreads();\n    STAMP(13);\n    if (tid == 0) stSc1(G(A().arrive) + it.i, A().epoch);"),
+    ("codec.hip", "uint32_t deviceErrorCount(bool reset) {", "extern \"C\" void* dietgpu_debug_stamps() { void* p = nullptr; (void)hipGetSymbolAddress(&p, HIP_SYMBOL(g_stamp)); return p; }\n\nuint32_t deviceErrorCount(bool reset) {"),
+]
+def STAG(ticks):
+    return [(P, "  if (iL >= A().items) return;\n", "  if (iL >= A().items) return;\n  if (A().xcdTeams && (((blockIdx.x >> 3) / A().team) & 1)) {\n    const unsigned long long t0_ = __builtin_amdgcn_s_memrealtime();\n    while (__builtin_amdgcn_s_memrealtime() - t0_ < %dull) __builtin_amdgcn_s_sleep(8);\n  }\n" % ticks)]
+NTLD = [(P, "      pv[g % D][k] = ld16(j0 < uw ? src + j0 : elem);", "      { const u32x4 v_ = __builtin_nontemporal_load((gp<const u32x4>)(j0 < uw ? src + j0 : elem)); pv[g % D][k] = make_uint4(v_.x, v_.y, v_.z, v_.w); }")]
+NTST = [("encode.h", "    if (store) st8(raw + i0, make_uint2(r0, r1));", "    if (store) __builtin_nontemporal_store(u32x2{r0, r1}, (gp<u32x2>)(raw + i0));")]
+PRIO = [(P, "    // E's word counts and L's histogram counts are in; E's aggregate goes out", "    __builtin_amdgcn_s_setprio(3);\n    // E's word counts and L's histogram counts are in; E's aggregate goes out"),
+        (P, "    if (!hasE && !hasL) break;\n", "    if (!hasE && !hasL) break;\n    __builtin_amdgcn_s_setprio(0);\n")]
+def STAG4(ticks):
+    return [(P, "  if (iL >= A().items) return;\n", "  if (iL >= A().items) return;\n  {\n    const unsigned long long t0_ = __builtin_amdgcn_s_memrealtime();\n    const unsigned long long dl_ = (blockIdx.x >> 8) * %dull;\n    while (__builtin_amdgcn_s_memrealtime() - t0_ < dl_) __builtin_amdgcn_s_sleep(8);\n  }\n" % ticks)]
+SP = "sparse.hip"
+VARS = {
+    "encprio": [("encode.h", "    // every wave's slot stores are complete before other waves copy them\n    asm volatile(\"s_waitcnt vmcnt(0)\" ::: \"memory\");", "    __builtin_amdgcn_s_setprio(2);\n    // every wave's slot stores are complete before other waves copy them\n    asm volatile(\"s_waitcnt vmcnt(0)\" ::: \"memory\");")],
+    "d3": [(P, "  constexpr int D = 2;", "  constexpr int D = 3;")],
+    "sp_nolb": [(SP, "    const uint32_t excl =\n        lookBackPoison(G(flags) + uint64_t(b) * tilesPerElem, tile, total, epoch, spinCap, pz);", "    const uint32_t excl = tile * 409u; (void)total;")],
+    "sp_nowr": [(SP, "      list[dst] = W(0);\n      if (v != W(0)) list[dst + 1] = v;\n    } else if (v != W(0)) {\n      list[dst] = v;\n    }", "      (void)dst;\n    } else if (v == W(0x12345u)) {\n      list[dst] = v;\n    }")],
+    "st4a": STAG4(300),
+    "st4b": STAG4(600),
+    "st4c": STAG4(900),
+    "prio": PRIO,
+    "prio2": [(PRIO[0][0], PRIO[0][1], PRIO[0][2].replace("setprio(3)", "setprio(2)")), PRIO[1]],
+    "nopc": [("codec.hip", "  if (team > pc::kMaxTeam) return false;", "  if (team > 0) return false;")],
+    "ntld": NTLD,
+    "ntst": NTST,
+    "ntldst": NTLD + NTST,
+    "stag5": STAG(500),
+    "stag10": STAG(1000),
+    "stag16": STAG(1600),
+    "stamp2": STAMP2,
+    "stamp": STAMP,
+    "noenc_nohist": [NOENC] + NOHIST,
+    "noenc_nohist_nosplitst": [NOENC, NOSPLITST] + NOHIST,
+    "noenc_nonorm": [NOENC] + NONORM,
+    "noenc_nohist_nonorm_nosplitst": [NOENC, NOSPLITST] + NOHIST + NONORM,
+    "base": [],
+    "hist2x": [(P, "__hip_atomic_fetch_add(hcol + __umul24(sym, pc::kHistStride), 1u, __ATOMIC_RELAXED,\n                               __HIP_MEMORY_SCOPE_WORKGROUP);",
+                "__hip_atomic_fetch_add(hcol + __umul24(sym, pc::kHistStride), 1u, __ATOMIC_RELAXED,\n                               __HIP_MEMORY_SCOPE_WORKGROUP);\n        __hip_atomic_fetch_add(hcol + __umul24(sym, pc::kHistStride), 1u, __ATOMIC_RELAXED,\n                               __HIP_MEMORY_SCOPE_WORKGROUP);")],
+    "nowait": [(P, "bool ok = it.team == 1;", "bool ok = true;"),
+               (P, "G(A().part) + uint64_t(it.tb) * kNumSymbols + tid;", "G(A().part) + uint64_t(it.i) * kNumSymbols + tid;"),
+               (P, "for (uint32_t k0 = 0; k0 < it.team; k0 += 16) {", "for (uint32_t k0 = 0; k0 < 1; k0 += 16) {"),
+               (P, "acc[k] = k0 + k < it.team ?", "acc[k] = k0 + k < 1 ?"),
+               (P, "const uint32_t q = it.n == 0 ? 0u : normalizeCount(count, it.n, A().pb, keys, red);",
+                   "const uint32_t ownN = it.x * 32768u < it.n ? min(it.n - it.x * 32768u, 32768u) : 0u;\n    const uint32_t q = ownN == 0 ? 0u : normalizeCount(count, ownN, A().pb, keys, red);")],
+    "noenc": [(P, "const bool encOn = hasE && uwE0 != 0 && !poisonE;", "const bool encOn = false;")],
+    "noplace": [(P, "for (uint32_t v = tid; v < nv; v += pc::kThreads) {", "for (uint32_t v = tid; v < nv && nv == 0xFFFFFFFFu; v += pc::kThreads) {")],
+    "nosplitst": [(P, "splitVec<FT>(v, i0, it.n, raw, myT + off, myT + off, store);", "splitVec<FT>(v, i0, it.n, raw, myT + off, myT + off, false);")],
+}
+for name in sys.argv[1:]:
+    root = f"/tmp/var/{name}"
+    shutil.rmtree(root, ignore_errors=True)
+    os.makedirs(f"{root}/dietgpu_fork_amd")
+    shutil.copytree(f"{REPO}/dietgpu_fork_amd/csrc", f"{root}/dietgpu_fork_amd/csrc")
+    os.symlink(f"{REPO}/include", f"{root}/include")
+    for f, a, b in VARS[name]:
+        p = f"{root}/dietgpu_fork_amd/csrc/{f}"
+        s = open(p).read()
+        n = s.count(a)
+        assert n >= 1, (name, a[:60])
+        open(p, "w").write(s.replace(a, b))
+    subprocess.check_call(["make", "-s", "-j8", "-C", f"{root}/dietgpu_fork_amd/csrc", "../_lib/libdietgpu_amd.so"])
+    shutil.copy(f"{root}/dietgpu_fork_amd/_lib/libdietgpu_amd.so", f"{REPO}/tools/ablibs/{name}.so")
+    print("built", name)
