@@ -86,7 +86,7 @@ def main():
     else:
         nb = args.batch
         total = nb * world
-        g = torch.Generator(device=dev).manual_seed(1000 + rank)
+        g = torch.Generator(device=dev).manual_seed(rank)  # seed 0
         x32 = torch.randn(nb, n, generator=g, device=dev, dtype=torch.float32)
         x = (x32.view(torch.int32) >> 16).to(torch.int16).view(torch.bfloat16)  # truncation
         del x32
@@ -231,13 +231,13 @@ def main():
 
 def _bf16_rows(first, last, n, dev, chunk=512):
     """Rows [first, last) of the c5 batch: N(0,1) fp32 truncated to bf16, the
-    rows of chunk c drawn from seed 5000 + c, so every row's contents are the
-    same whatever the sharding."""
+    rows of chunk c drawn from seed c (seed 0 for the first
+    chunk), so every row's contents are the same whatever the sharding."""
     import torch
 
     x = torch.empty([last - first, n], dtype=torch.bfloat16, device=dev)
     for c in range(first // chunk, -(-last // chunk)):
-        g = torch.Generator(device=dev).manual_seed(5000 + c)
+        g = torch.Generator(device=dev).manual_seed(c)
         x32 = torch.randn(chunk, n, generator=g, device=dev, dtype=torch.float32)
         a, b = max(first, c * chunk), min(last, (c + 1) * chunk)
         rows = (x32[a - c * chunk:b - c * chunk].view(torch.int32) >> 16).to(torch.int16)
@@ -469,7 +469,18 @@ def _cpu_baseline(x, sample, pb, min_seconds=12.0, max_passes=40):
                       f"{passes} passes of compress+decompress, serial C oracle "
                       f"(oracle/dietgpu_oracle.c), 1 thread",
             "seconds": round(tot, 3), "compress_s": round(te_s, 3), "decompress_s": round(td_s, 3),
-            "ratio": round(comp / U, 5), "host_cpus": os.cpu_count()}
+            "ratio": round(comp / U, 5), "host_cpus": os.cpu_count(), "host_cpu_model": _cpu_model()}
+
+
+def _cpu_model():
+    """The host CPU's model name (report the lscpu model)."""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
 
 
 if __name__ == "__main__":
