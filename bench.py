@@ -190,7 +190,8 @@ def main():
         ach = algo[dominant] / (fam[dominant]["avg_ms"] * 1e-3) / 1e9
         roofline = {"bound": "hbm", "kernel": KERNEL_OF[dominant], "achieved": round(ach, 1),
                     "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBPS, 4),
-                    "traffic": _pmc_traffic(dominant, ft),
+                    # PMC traffic is profiled on c2 (tools/profile_gpu.sh)
+                    "traffic": _pmc_traffic(dominant, ft) if workload == "c2" else None,
                     "algorithmic_bytes_per_launch": algo[dominant]}
     t_enc = sum(fam[k]["avg_ms"] for k in ("compress", "hist", "normalize", "encode", "coalesce") if k in fam)
     t_dec = fam.get("decode", {}).get("avg_ms", 0.0)
