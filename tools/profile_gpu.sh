@@ -5,7 +5,7 @@
 #   usage: bash tools/profile_gpu.sh <tag> [bench args...]
 set -e
 TAG=${1:-r01}; shift || true
-ARGS=${*:-"--steps 10 --warmup 3 --no-cpu-baseline --no-extras"}
+ARGS=${*:-"--no-cpu-baseline --no-extras"}
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 OUT=gpurun_out/prof_$TAG
