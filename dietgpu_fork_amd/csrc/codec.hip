@@ -369,12 +369,14 @@ void encodeBatchDevice(StackDeviceMemory& res, int pb, bool useChecksum, uint32_
 template <int FT>
 void decodeBatchDevice(StackDeviceMemory& res, int pb, uint32_t nb, const BatchDesc& in,
                        const BatchDesc& out, uint32_t maxCapacity, uint8_t* outSuccess_dev,
-                       uint32_t* outSize_dev, hipStream_t s, const DeviceTables* tabs = nullptr) {
+                       uint32_t* outSize_dev, hipStream_t s, const DeviceTables* tabs = nullptr,
+                       bool streamOut = true) {
   checkProbBits(pb);
   if (nb == 0) return;
   const uint32_t maxBlocks = divUp(maxCapacity, kBlockSize);
-  auto launch = [&](auto kTag) {
+  auto launch = [&](auto kTag, auto ntTag) {
     constexpr int KK = decltype(kTag)::value;
+    constexpr bool NT = decltype(ntTag)::value;
     using Cfg = DecCfg<FT, KK>;
     for (uint32_t y0 = 0; y0 < nb; y0 += kMaxGridY) {
       const uint32_t ny = std::min(kMaxGridY, nb - y0);
@@ -383,15 +385,20 @@ void decodeBatchDevice(StackDeviceMemory& res, int pb, uint32_t nb, const BatchD
       const uint32_t lds = Cfg::ldsBytes(pb);
       const uint32_t chunks = std::max(1u, divUp(maxBlocks, Cfg::kBlocksPerWG));
       const uint32_t slots =
-          residentSlots(reinterpret_cast<const void*>(&k_decode<FT, KK>), dec::kThreads, lds);
+          residentSlots(reinterpret_cast<const void*>(&k_decode<FT, KK, NT>), dec::kThreads, lds);
       const uint32_t P = std::max(1u, uint32_t((uint64_t(chunks) * ny + slots / 2) / slots));
       dim3 g(divUp(chunks, P), ny);
-      k_decode<FT, KK><<<g, dec::kThreads, lds, s>>>(kernargTable(tabs), in, out, y0, pb, P,
-                                                     outSuccess_dev, outSize_dev);
+      k_decode<FT, KK, NT><<<g, dec::kThreads, lds, s>>>(kernargTable(tabs), in, out, y0, pb, P,
+                                                         outSuccess_dev, outSize_dev);
       HIP_LAUNCH_CHECK();
     }
   };
-  launch(std::integral_constant<int, 0>{});
+  // streaming stores when nobody re-reads the output right away (fp64's
+  // 8-dword rows measured slower with them)
+  if constexpr (FT != 4) {
+    if (streamOut) return launch(std::integral_constant<int, 0>{}, std::true_type{});
+  }
+  launch(std::integral_constant<int, 0>{}, std::false_type{});
 }
 
 // Verify stored checksums against `unitBytes * out.size(b)` decoded bytes
@@ -527,7 +534,7 @@ static ANSDecodeStatus ansDecodeCommon(StackDeviceMemory& res, const ANSCodecCon
                                        uint32_t maxCap, uint8_t* succ, uint32_t* sizes,
                                        hipStream_t s, const DeviceTables* tabs = nullptr) {
   ANSDecodeStatus status;
-  decodeBatchDevice<0>(res, config.probBits, nb, in, out, maxCap, succ, sizes, s, tabs);
+  decodeBatchDevice<0>(res, config.probBits, nb, in, out, maxCap, succ, sizes, s, tabs, !config.useChecksum);
   if (config.useChecksum) {
     status.errorInfo = verifyChecksums(res, nb, in, false, out, maxCap, s, tabs);
     if (!status.errorInfo.empty()) status.error = ANSDecodeError::ChecksumMismatch;
@@ -665,21 +672,23 @@ FloatDecompressStatus floatDecompressDescs(StackDeviceMemory& res,
                                            const FloatDecompressConfig& config, uint32_t nb,
                                            const BatchDesc& in, const BatchDesc& out,
                                            uint32_t maxCap, uint8_t* succ, uint32_t* sizes,
-                                           hipStream_t s, const DeviceTables* tabs) {
+                                           hipStream_t s, const DeviceTables* tabs, bool streamOut) {
   checkFloatConfig(config);
   const int pb = config.ansConfig.probBits;
+  // streaming output stores unless the output is read back (checksum)
+  const bool nt = streamOut && !config.useChecksum;
   switch (config.floatType) {
     case FloatType::kFloat16:
-      decodeBatchDevice<1>(res, pb, nb, in, out, maxCap, succ, sizes, s, tabs);
+      decodeBatchDevice<1>(res, pb, nb, in, out, maxCap, succ, sizes, s, tabs, nt);
       break;
     case FloatType::kBFloat16:
-      decodeBatchDevice<2>(res, pb, nb, in, out, maxCap, succ, sizes, s, tabs);
+      decodeBatchDevice<2>(res, pb, nb, in, out, maxCap, succ, sizes, s, tabs, nt);
       break;
     case FloatType::kFloat32:
-      decodeBatchDevice<3>(res, pb, nb, in, out, maxCap, succ, sizes, s, tabs);
+      decodeBatchDevice<3>(res, pb, nb, in, out, maxCap, succ, sizes, s, tabs, nt);
       break;
     default:
-      decodeBatchDevice<4>(res, pb, nb, in, out, maxCap, succ, sizes, s, tabs);
+      decodeBatchDevice<4>(res, pb, nb, in, out, maxCap, succ, sizes, s, tabs, nt);
       break;
   }
   FloatDecompressStatus status;

@@ -21,7 +21,8 @@ FloatDecompressStatus floatDecompressDescs(StackDeviceMemory& res,
                                            const FloatDecompressConfig& config, uint32_t nb,
                                            const BatchDesc& in, const BatchDesc& out,
                                            uint32_t maxCap, uint8_t* succ, uint32_t* sizes,
-                                           hipStream_t s, const DeviceTables* tabs = nullptr);
+                                           hipStream_t s, const DeviceTables* tabs = nullptr,
+                                           bool streamOut = true);
 
 // Compare archive checksums with the XOR of `decoded.size(b)` bytes of each
 // decoded element; synchronises `s`.

@@ -244,13 +244,22 @@ struct Join {
     return __builtin_amdgcn_perm(sp, rw, odd ? 0x07030502u : 0x07010500u);
   }
 
-  // vector join of a full chunk: out words [i0, i0 + 8).  s / s1: 4 dwords of
+  // vector join of a full chunk: out words [i0, i0 + 8).  nt: streaming
+  // stores (the decoded output is not read again by the codec; not for fp64,
+  // whose lanes write 64 B each in four stores: streaming partial lines
+  // measured 2.5x slower).  s / s1: 4 dwords of
   // u16 (sym << 8) of stream 0 / 1.
+  // NT: streaming (non-temporal) stores.  A compile-time choice: with a
+  // runtime flag LLVM sinks the two stores of each branch into one and drops
+  // the nontemporal hint.
+  template <bool nt>
   static __device__ __forceinline__ void vec(gp<uint8_t> outB, uint32_t i0, const uint32_t (&s)[4],
                                              const uint32_t (&s1)[4], const uint32_t (&r)[kR]) {
     if constexpr (FT == 0) {
-      st8(outB + i0, make_uint2(__builtin_amdgcn_perm(s[1], s[0], 0x07050301u),
-                                __builtin_amdgcn_perm(s[3], s[2], 0x07050301u)));
+      const uint2 v = make_uint2(__builtin_amdgcn_perm(s[1], s[0], 0x07050301u),
+                                 __builtin_amdgcn_perm(s[3], s[2], 0x07050301u));
+      if constexpr (nt) st8nt(outB + i0, v);
+      else st8(outB + i0, v);
     } else if constexpr (FT == 1 || FT == 2) {
       uint32_t o[4];
 #pragma unroll
@@ -259,7 +268,8 @@ struct Join {
         // bf16: rotate each 16-bit half right by one (raw = mant << 1 | sign)
         o[k] = FT == 1 ? t : (((t >> 1) & 0x7fff7fffu) | ((t << 15) & 0x80008000u));
       }
-      st16(outB + 2 * i0, make_uint4(o[0], o[1], o[2], o[3]));
+      if constexpr (nt) st16nt(outB + 2 * i0, make_uint4(o[0], o[1], o[2], o[3]));
+      else st16(outB + 2 * i0, make_uint4(o[0], o[1], o[2], o[3]));
     } else if constexpr (FT == 3) {
       uint32_t o[8];
 #pragma unroll
@@ -271,8 +281,13 @@ struct Join {
         o[2 * k + 1] = __builtin_amdgcn_alignbit(w1, w1, 1);
       }
       gp<uint4> d = (gp<uint4>)(outB + 4 * i0);
-      st16(d, make_uint4(o[0], o[1], o[2], o[3]));
-      st16(d + 1, make_uint4(o[4], o[5], o[6], o[7]));
+      if constexpr (nt) {
+        st16nt(d, make_uint4(o[0], o[1], o[2], o[3]));
+        st16nt(d + 1, make_uint4(o[4], o[5], o[6], o[7]));
+      } else {
+        st16(d, make_uint4(o[0], o[1], o[2], o[3]));
+        st16(d + 1, make_uint4(o[4], o[5], o[6], o[7]));
+      }
     } else {
       gp<uint4> d = (gp<uint4>)(outB + 8 * i0);
 #pragma unroll
@@ -315,7 +330,7 @@ __device__ __forceinline__ void buildLut64(gp<const uint16_t> pdfIn, lp<u32x2> l
 // DecCfg<FT>::ldsBytes(pb).  out.size(b) = capacity (bytes for raw ANS,
 // words for floats).  Pointer tables may ride in the first (InlineTable) argument
 // (BatchDesc::field).
-template <int FT, int KK>
+template <int FT, int KK, bool NT>
 __global__ __launch_bounds__(dec::kThreads) void k_decode(const InlineTable,
                                                           BatchDesc in, BatchDesc out,
                                                           uint32_t batchOffset, int pb,
@@ -504,7 +519,7 @@ __global__ __launch_bounds__(dec::kThreads) void k_decode(const InlineTable,
 #pragma unroll
               for (int k = 0; k < 4; ++k) sv1[k] = 0;
             }
-            Join<FT>::vec(outB, i0, sv, sv1, rv[c]);
+            Join<FT>::template vec<NT>(outB, i0, sv, sv1, rv[c]);
           } else {
             gp<WordT> o = (gp<WordT>)outB;
             for (uint32_t k = 0; k < cnt; ++k)

@@ -45,6 +45,19 @@ __device__ __forceinline__ uint2 ld8(gp<const void> p) {
 __device__ __forceinline__ void st8(gp<void> p, uint2 v) {
   *(gp<u32x2>)p = u32x2{v.x, v.y};
 }
+// Streaming variants (non-temporal): for data read or written exactly once in
+// a call -- the compressor's input, the decompressor's output -- so that the
+// caches (L2, MALL) keep the archives, which the other direction reads next.
+__device__ __forceinline__ uint4 ld16nt(gp<const void> p) {
+  const u32x4 v = __builtin_nontemporal_load((gp<const u32x4>)p);
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void st16nt(gp<void> p, uint4 v) {
+  __builtin_nontemporal_store(u32x4{v.x, v.y, v.z, v.w}, (gp<u32x4>)p);
+}
+__device__ __forceinline__ void st8nt(gp<void> p, uint2 v) {
+  __builtin_nontemporal_store(u32x2{v.x, v.y}, (gp<u32x2>)p);
+}
 
 template <int FT>
 struct FloatTraits;

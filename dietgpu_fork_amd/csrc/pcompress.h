@@ -244,7 +244,10 @@ __global__ __launch_bounds__(pc::kThreads) __attribute__((amdgpu_waves_per_eu(4,
            uint64_t(it.x * pc::kBlocksPerItem + 2 * w + h) * kBlockSize;
   };
 
-  // 16 B loads of segment g of this lane's block, issued unconditionally (an
+  // 16 B streaming loads of segment g of this lane's block (the input is read
+  // once; non-temporal, so the caches keep the archives for the decoder:
+  // c2 step 267 -> 239 us together with the decoder's streaming stores,
+  // same-box A/B), issued unconditionally (an
   // item's load schedule is then branch-free, so the compiler's wait counts
   // stay exact instead of draining every load in flight at a branch merge):
   // a vector with no word of the block reads the element's first vector
@@ -256,7 +259,7 @@ __global__ __launch_bounds__(pc::kThreads) __attribute__((amdgpu_waves_per_eu(4,
 #pragma unroll
     for (int k = 0; k < V; ++k) {
       const uint32_t j0 = g * pc::kSegWords + (k * 32 + l) * kWPV;
-      pv[g % D][k] = ld16(j0 < uw ? src + j0 : elem);
+      pv[g % D][k] = ld16nt(j0 < uw ? src + j0 : elem);
     }
   };
 

@@ -378,7 +378,7 @@ FloatDecompressStatus sparseDecompressT(StackDeviceMemory& res,
   cfg.useChecksum = false;
   floatDecompressDescs(res, cfg, nb, BatchDesc::pointers(densePtrs.data(), nullptr),
                        BatchDesc::pointers(listPtrsDev.data(), nullptr, maxCap + 1), maxCap + 1,
-                       denseOk.data(), nullptr, s);
+                       denseOk.data(), nullptr, s, nullptr, /*streamOut=*/false);  // the expansion reads it
   FloatDecompressStatus status;
   if (config.useChecksum) {
     // verify the dense archive's checksum over the bytes it was computed on
