@@ -239,3 +239,29 @@ def test_sparse_all_zero_and_dense(C, ws):
     C.sparse_decompress(arch, outs, ft=ft, ws=ws)
     for w, o in zip(ws_, outs):
         np.testing.assert_array_equal(to_np_words(o, ft), w)
+
+
+@pytest.mark.parametrize("ft", [2, 3])
+def test_sparse_large_lists(C, ws, ft):
+    """Nonzero lists from empty to fully dense in one batch of 3 M-word
+    elements (the dense codec's multi-chunk histogram path over lists whose
+    lengths only the device knows)."""
+    n = 3 << 20
+    fracs = [0.9, 0.0, 0.5, 1.0, 0.999]
+    words = [sparsify(float_words(ft, n, seed=70 + i), f, seed=80 + i) for i, f in enumerate(fracs)]
+    ts = [to_dev_words(w, ft) for w in words]
+    out, sizes = C.sparse_compress(ts, ft=ft, ws=ws)
+    host = out.cpu().numpy()
+    sizes_h = sizes.cpu().tolist()
+    assert C.device_error_count(reset=True) == 0
+    for i, w in enumerate(words):
+        ref = O.sparse_compress(w, ft)
+        assert sizes_h[i] == ref.size, (i, sizes_h[i], ref.size)
+        np.testing.assert_array_equal(host[i, : ref.size], ref, err_msg=f"element {i}")
+    arch = [out[i, : sizes_h[i]].clone() for i in range(len(ts))]
+    del out
+    outs = [torch.empty(n, dtype=TORCH_WORD[ft], device=DEV) for _ in words]
+    ok, sz = C.sparse_decompress(arch, outs, ft=ft, ws=ws)
+    assert ok.cpu().tolist() == [1] * len(ts)
+    for w, o in zip(words, outs):
+        np.testing.assert_array_equal(to_np_words(o, ft), w)

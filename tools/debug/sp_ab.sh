@@ -1,2 +1,10 @@
-for L in cur rts cur rts; do cp tools/ablibs/$L.so dietgpu_fork_amd/_lib/libdietgpu_amd.so; echo -n "$L: "; timeout -k 10 60 python tools/debug/sparse_bench.py 50 || exit 1; done
-cp tools/ablibs/rts.so dietgpu_fork_amd/_lib/libdietgpu_amd.so
+#!/bin/bash
+# GPU box: sparse c4 timings of variant libraries, back to back.
+#   usage: bash tools/debug/sp_ab.sh <a.so> <b.so> ...
+LIB=dietgpu_fork_amd/_lib/libdietgpu_amd.so
+cp "$LIB" /tmp/sp_default.so
+for L in "$@"; do
+  cp "$L" "$LIB"; echo -n "$(basename "$L" .so): "
+  timeout -k 10 60 python tools/debug/sparse_bench.py 50 || { cp /tmp/sp_default.so "$LIB"; exit 1; }
+done
+cp /tmp/sp_default.so "$LIB"
