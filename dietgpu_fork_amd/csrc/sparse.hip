@@ -62,7 +62,7 @@ __device__ __forceinline__ void loadTile(gp<const W> x, uint32_t t0, uint32_t ti
       const uint32_t wi = (v * kThreads + tid) * kWPV;  // first word of the vector
       uint4 val = make_uint4(0, 0, 0, 0);
       if (wi + kWPV <= tileN) {
-        val = ld16((gp<const uint4>)(x + t0 + wi));
+        val = ld16nt((gp<const uint4>)(x + t0 + wi));  // read once: stream it
       } else if (wi < tileN) {
         W tmp[kWPV];
 #pragma unroll
@@ -105,26 +105,32 @@ __global__ __launch_bounds__(kThreads) void k_sparseCount(BatchDesc in, const ui
     return;
   }
   gp<const W> x = (gp<const W>)in.start(b);
+  // bitwise: -0.0 is "nonzero" (generate_bitmap :56); loaded with the tile
+  const W xn2 = n >= 2 ? x[n - 2] : W(1);
   loadTile<W, kVec>(x, t0, min(kTileWords, n - t0), buf);
   __syncthreads();
   const uint32_t bmBytes = (n + 7) / 8, bmPad = roundUp(bmBytes, 16);
-  // bitwise: -0.0 is "nonzero" (generate_bitmap :56)
-  const bool gap = n >= 2 && x[n - 2] == W(0);
+  const bool gap = xn2 == W(0);
   uint64_t m[kSteps];
   uint32_t cnt = 0;
+  uint64_t bmLane = 0;  // lane j < kSteps: the bitmap word of step j
 #pragma unroll
   for (uint32_t j = 0; j < kSteps; ++j) {
     const uint32_t q = w * (kTileWords / kWaves) + 64 * j;  // step's first word in the tile
     m[j] = ballot(buf[q + lane] != W(0));
     cnt += uint32_t(__popcll(m[j]));
+    bmLane = lane == j ? maskToBitmap(m[j]) : bmLane;
     const uint32_t i0 = t0 + q;
-    if (lane == 0 && i0 < n) {
-      gp<uint64_t> dst = (gp<uint64_t>)(o + 16 + i0 / 8);
-      dst[0] = maskToBitmap(m[j]);
-      // zero the 16-byte padding after the last bitmap word
-      const uint32_t end = i0 / 8 + 8;
-      if (i0 + 64 >= n && end < bmPad) dst[1] = 0;
-      if (gap && i0 <= n - 1 && n - 1 < i0 + 64) cnt += 1;  // the extra slot
+    if (gap && i0 <= n - 1 && n - 1 < i0 + 64) cnt += 1;  // the extra slot
+  }
+  {
+    // the wave's kSteps bitmap words in one store; then zero the 16-byte
+    // padding after the element's last bitmap word
+    const uint32_t i0 = t0 + w * (kTileWords / kWaves) + 64 * lane;
+    gp<uint64_t> dst = (gp<uint64_t>)(o + 16 + i0 / 8);
+    if (lane < kSteps && i0 < n) {
+      dst[0] = bmLane;
+      if (i0 + 64 >= n && i0 / 8 + 8 < bmPad) dst[1] = 0;
     }
   }
   if (lane == 0) waveCnt[w] = cnt;
