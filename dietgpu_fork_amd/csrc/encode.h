@@ -354,6 +354,10 @@ constexpr int kWaves = kThreads / 64;
 constexpr uint32_t kSegSteps = 16;
 constexpr uint32_t kSegWords = kSegSteps * 32;
 constexpr uint32_t kRing = 512;    // u16 words per block-stream output ring
+// Single-segment formats keep a block's whole typical output in LDS (a 4 KiB
+// block at 4 bit/symbol is ~1.1 K words): only overflow beyond the ring goes
+// through the slot, the rest is copied from LDS straight to its final place
+constexpr uint32_t kRingFused = 1024;
 constexpr uint32_t kFlush = 256;   // words per flush (64 lanes x 8 B)
 constexpr uint32_t kUnroll = 4;    // steps between flush checks
 }  // namespace enc
@@ -544,8 +548,14 @@ __device__ __forceinline__ void splitOne(typename FloatTraits<FT>::WordT w, uint
 // every thread copies 16 B vectors (8 words) across the whole range, the
 // source slot found by binary search over pre; 4 vectors in flight per
 // thread.  Words past a block's count are written as 0.
+// With rings (k_encode, single-segment formats): words at or past flushed[k]
+// are still in block k's LDS ring (rings + k * kR, index mod kR; flushed is a
+// multiple of 256 and the vectors 8-word aligned, so a vector never straddles).
+template <uint32_t kR = 0>
 __device__ __forceinline__ void copyPayload(const uint32_t* pre, const uint32_t* cwL, uint32_t nk,
-                                            gp<const uint8_t> slot0, gp<uint8_t> data) {
+                                            gp<const uint8_t> slot0, gp<uint8_t> data,
+                                            const uint16_t* rings = nullptr,
+                                            const uint32_t* flushed = nullptr) {
   if (nk == 0) return;
   const uint32_t tid = threadIdx.x;
   const uint32_t w0 = pre[0];
@@ -568,7 +578,12 @@ __device__ __forceinline__ void copyPayload(const uint32_t* pre, const uint32_t*
         }
         const uint32_t off = w - pre[lo];
         valid[q] = cwL[lo] > off ? cwL[lo] - off : 0;
-        val[q] = ld16((gp<const uint4>)(slot0 + uint64_t(lo) * kSlotBytes + 2ull * off));
+        if (kR && off >= flushed[lo]) {
+          const u32x4 r = *(lp<const u32x4>)(rings + lo * kR + (off & (kR - 1)));
+          val[q] = make_uint4(r[0], r[1], r[2], r[3]);
+        } else {
+          val[q] = ld16((gp<const uint4>)(slot0 + uint64_t(lo) * kSlotBytes + 2ull * off));
+        }
       }
     }
 #pragma unroll
@@ -734,12 +749,15 @@ __global__ __launch_bounds__(enc::kThreads) void k_encode(BatchDesc in, BatchDes
   using Cfg = EncCfg<FT, KK>;
   using WordT = typename Cfg::WordT;
   constexpr int S = Cfg::S, K = Cfg::K, V = Cfg::V;
+  constexpr bool kFused = S == 1;
+  constexpr uint32_t R = kFused ? enc::kRingFused : enc::kRing;
+  static_assert(!kFused || K == 1, "fused copy addresses block k's ring at k * R");
   __shared__ __attribute__((aligned(16))) uint32_t tblS[S][kNumSymbols * 4];
   __shared__ __attribute__((aligned(16))) uint8_t symS[Cfg::kHalfStreams][enc::kSegWords];
-  __shared__ __attribute__((aligned(16))) uint16_t ringS[Cfg::kHalfStreams / 2][2 * enc::kRing];
+  __shared__ __attribute__((aligned(16))) uint16_t ringS[Cfg::kHalfStreams / 2][2 * R];
   __shared__ uint32_t trashS[enc::kWaves][64];
-  constexpr bool kFused = S == 1;
   __shared__ uint32_t cwE[Cfg::kBlocksPerWG];
+  __shared__ uint32_t flE[Cfg::kBlocksPerWG];
   __shared__ uint32_t preE[Cfg::kBlocksPerWG];
 
   const uint32_t b = batchOffset + blockIdx.y;
@@ -790,7 +808,7 @@ __global__ __launch_bounds__(enc::kThreads) void k_encode(BatchDesc in, BatchDes
       const uint32_t hs = (w * K + c) * S + s;
       p.x = kStartState;
       p.ring = (lp<uint16_t>)&ringS[hs][0];
-      p.ringLane = p.ring + (hv & enc::kRing);
+      p.ringLane = p.ring + (hv & R);
       symLane[c][s] = (lp<uint8_t>)&symS[2 * hs][0] + (hv & enc::kSegWords) + l;
 #pragma unroll
       for (int hh = 0; hh < 2; ++hh) {
@@ -864,7 +882,7 @@ __global__ __launch_bounds__(enc::kThreads) void k_encode(BatchDesc in, BatchDes
 #pragma unroll
       for (int c = 0; c < K; ++c)
 #pragma unroll
-        for (int s = 0; s < S; ++s) ringFlush<256>(st[c][s], lane);
+        for (int s = 0; s < S; ++s) ringFlush<int(R - 256), R>(st[c][s], lane);
       if (g + 1 < nSeg) loadSeg(g + 1);
       __builtin_amdgcn_wave_barrier();
 #pragma unroll
@@ -872,7 +890,7 @@ __global__ __launch_bounds__(enc::kThreads) void k_encode(BatchDesc in, BatchDes
 #pragma unroll
         for (int c = 0; c < K; ++c)
 #pragma unroll
-          for (int s = 0; s < S; ++s) ringFlush<384>(st[c][s], lane);
+          for (int s = 0; s < S; ++s) ringFlush<int(R - 128), R>(st[c][s], lane);
         // the group's symbols and table entries first: their LDS reads
         // cannot be hoisted over the ring stores of earlier steps
         u32x4 E[enc::kUnroll][K][S];
@@ -888,7 +906,7 @@ __global__ __launch_bounds__(enc::kThreads) void k_encode(BatchDesc in, BatchDes
 #pragma unroll
           for (int c = 0; c < K; ++c)
 #pragma unroll
-            for (int s = 0; s < S; ++s) encStep<false>(st[c][s], true, E[u][c][s], hv, trashAddr);
+            for (int s = 0; s < S; ++s) encStep<false, R>(st[c][s], true, E[u][c][s], hv, trashAddr);
       }
       __builtin_amdgcn_wave_barrier();
     }
@@ -898,7 +916,7 @@ __global__ __launch_bounds__(enc::kThreads) void k_encode(BatchDesc in, BatchDes
 #pragma unroll
       for (int c = 0; c < K; ++c)
 #pragma unroll
-        for (int s = 0; s < S; ++s) ringFlush<256>(st[c][s], lane);
+        for (int s = 0; s < S; ++s) ringFlush<int(R - 256), R>(st[c][s], lane);
       if (g + 1 < nSeg) loadSeg(g + 1);
       __builtin_amdgcn_wave_barrier();
       const uint32_t tEnd = min(T, (g + 1) * enc::kSegSteps);
@@ -906,7 +924,7 @@ __global__ __launch_bounds__(enc::kThreads) void k_encode(BatchDesc in, BatchDes
 #pragma unroll
         for (int c = 0; c < K; ++c)
 #pragma unroll
-          for (int s = 0; s < S; ++s) ringFlush<int(512 - 32)>(st[c][s], lane);
+          for (int s = 0; s < S; ++s) ringFlush<int(R - 32), R>(st[c][s], lane);
         const uint32_t tr = t - g * enc::kSegSteps;
 #pragma unroll
         for (int c = 0; c < K; ++c) {
@@ -915,7 +933,7 @@ __global__ __launch_bounds__(enc::kThreads) void k_encode(BatchDesc in, BatchDes
           for (int s = 0; s < S; ++s) {
             const uint32_t sym = valid ? uint32_t(symLane[c][s][tr * 32]) : 0u;
             const u32x4 e = tbl[s][sym];
-            encStep<true>(st[c][s], valid, e, hv, trashAddr);
+            encStep<true, R>(st[c][s], valid, e, hv, trashAddr);
           }
         }
       }
@@ -932,12 +950,15 @@ __global__ __launch_bounds__(enc::kThreads) void k_encode(BatchDesc in, BatchDes
 #pragma unroll
     for (int s = 0; s < S; ++s) {
       EStream& p = st[c][s];
-      ringFlushAll(p, lane);
+      if constexpr (!kFused) ringFlushAll(p, lane);  // fused: the rest stays in LDS
       if (uw[c]) {
         const uint32_t words = uint32_t(h ? p.nout[1] : p.nout[0]);
         if constexpr (kFused) {
           ((gp<uint32_t>)(states + uint64_t(kStateBytesPerBlock) * blk[c]))[l] = p.x;
-          if (l == 0) cwE[blk[c] - first] = words;
+          if (l == 0) {
+            cwE[blk[c] - first] = words;
+            flE[blk[c] - first] = uint32_t(h ? p.flushed[1] : p.flushed[0]);
+          }
         } else {
           gp<uint8_t> slot = G(slots) + ((uint64_t(s) * numInBatch + b) * MB + blk[c]) * kSlotBytes;
           ((gp<uint32_t>)slot)[l] = p.x;
@@ -975,8 +996,8 @@ __global__ __launch_bounds__(enc::kThreads) void k_encode(BatchDesc in, BatchDes
       const uint32_t uwk = min(kBlockSize, n - k * kBlockSize);
       st8(bwords + k, make_uint2((uwk << 16) | cwE[tid], preE[tid]));
     }
-    copyPayload(preE, cwE, nk, G(slots) + (uint64_t(b) * MB + first) * kSlotBytes + kStateBytesPerBlock,
-                (gp<uint8_t>)(bwords + roundUp(nBlocks, 2)));
+    copyPayload<R>(preE, cwE, nk, G(slots) + (uint64_t(b) * MB + first) * kSlotBytes + kStateBytesPerBlock,
+                   (gp<uint8_t>)(bwords + roundUp(nBlocks, 2)), &ringS[0][0], flE);
   }
 }
 
