@@ -91,3 +91,15 @@ def test_float_unaligned_input(C, ws, offset_words):
     ref = O.float_compress(x.view(torch.int16).numpy().view(np.uint16), 2)
     assert int(sizes[0]) == ref.size
     np.testing.assert_array_equal(arch[0, : ref.size].cpu().numpy(), ref)
+
+
+@pytest.mark.parametrize("pb", [9, 11])
+def test_dense_blocks_three_kernel_ring_overflow(C, ws, pb):
+    """k_encode keeps each block's output in a 1024-word LDS ring and flushes
+    only the overflow to its slot: uniform bytes (~2048 words per block) wrap
+    the ring and spill several 256-word chunks; the > 1 MiB element sends the
+    whole batch down the three-kernel path."""
+    rng = np.random.default_rng(7)
+    datas = [rng.integers(0, 256, size=n, dtype=np.uint8) for n in (4096 * 24 + 77, 65536, 5000)]
+    datas.append(exp_bytes(MIB + 4096, lam=2.0, seed=23))
+    _check_ans(C, ws, datas, pb=pb)
