@@ -247,14 +247,21 @@ def _bf16_rows(first, last, n, dev, chunk=512):
     return x
 
 
-def _timed(fn, reps):
-    """Average ms of fn() over reps calls (torch events on the current stream,
-    which is the stream the C ABI launches on)."""
+def _timed(fn, reps, min_ms=2.0, max_reps=50):
+    """Average ms of fn() over back-to-back calls (torch events on the current
+    stream, which is the stream the C ABI launches on): at least `reps`, and
+    for short calls enough of them to cover ~min_ms, so the host's enqueue of
+    one call overlaps the GPU work of the previous one (steady state)."""
     import torch
 
     fn()
     torch.cuda.synchronize()
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    fn()
+    b.record()
+    b.synchronize()
+    reps = max(reps, min(max_reps, int(min_ms / max(a.elapsed_time(b), 1e-3)) + 1))
     a.record()
     for _ in range(reps):
         fn()
