@@ -336,17 +336,19 @@ static __global__ __launch_bounds__(kThreads) void k_normalize(
 // ---------------------------------------------------------------------------
 // k_encode: fused split + rANS encode.
 //   * 256-thread workgroups (4 waves).  Lanes 0-31 / 32-63 of a wave code
-//     one 4 KiB block each; each wave runs K block pairs (K = 2; fp64: K = 1
-//     with its two streams) as independent chains.
+//     one 4 KiB block each; each wave runs one block pair (fp64: with its
+//     two streams) as independent chains.
 //   * Per 512-symbol segment the wave splits 16 B input vectors (loaded one
 //     segment ahead): float raw bytes go straight to the archive's raw
 //     section, ANS symbols to LDS.  It then runs 16 branch-free encode steps
 //     per block from LDS (fully unrolled).
-//   * Emitted u16 words go to a 512-word LDS ring per block stream (writers
-//     at ascending lane order; non-writers store to a per-lane trash dword so
-//     the step has no branch); rings are flushed to the block's scratch slot
-//     256 words at a time with one 8 B store per lane.  k_coalesce packs the
-//     slots into the archive.
+//   * Emitted u16 words go to an LDS ring per block stream (writers at
+//     ascending lane order; non-writers store to a per-lane trash dword so
+//     the step has no branch).  fp64 (512-word rings): flushed to the block's
+//     scratch slot 256 words at a time with one 8 B store per lane, and
+//     k_coalesce packs the slots into the archive.  Single-segment formats
+//     (1024-word rings): only overflow is flushed; after the look-back the
+//     workgroup copies its blocks from the rings (and slots) to the archive.
 // ---------------------------------------------------------------------------
 namespace enc {
 constexpr int kThreads = 256;
