@@ -390,12 +390,20 @@ void decodeBatchDevice(StackDeviceMemory& res, int pb, uint32_t nb, const BatchD
       const uint32_t lds = Cfg::ldsBytes(pb);
       const uint32_t chunks = std::max(1u, divUp(maxBlocks, Cfg::kBlocksPerWG));
       const uint32_t slots =
-          residentSlots(reinterpret_cast<const void*>(&k_decode<FT, KK, NT>), dec::kThreads, lds);
+          residentSlots(reinterpret_cast<const void*>(&k_decode<FT, KK, NT, true>), dec::kThreads, lds);
       const uint32_t P = std::min(kMaxDecodeChunks,
                                   std::max(1u, uint32_t((uint64_t(chunks) * ny + slots / 2) / slots)));
       dim3 g(divUp(chunks, P), ny);
-      k_decode<FT, KK, NT><<<g, dec::kThreads, lds, s>>>(kernargTable(tabs), in, out, y0, pb, P,
-                                                         outSuccess_dev, outSize_dev);
+      // remaining-work wave priorities balance the finish of a single
+      // generation (c2 decode −2 %); across several generations they cost
+      // (c3 decode 2.02 ms without, 2.32 ms with, same-box A/B).  A template
+      // parameter: a runtime flag changed the step loop's code (c2 +25 %)
+      if (uint64_t(g.x) * ny <= slots)
+        k_decode<FT, KK, NT, true><<<g, dec::kThreads, lds, s>>>(kernargTable(tabs), in, out, y0, pb, P,
+                                                                 outSuccess_dev, outSize_dev);
+      else
+        k_decode<FT, KK, NT, false><<<g, dec::kThreads, lds, s>>>(kernargTable(tabs), in, out, y0, pb, P,
+                                                                  outSuccess_dev, outSize_dev);
       HIP_LAUNCH_CHECK();
     }
   };

@@ -330,7 +330,8 @@ __device__ __forceinline__ void buildLut64(gp<const uint16_t> pdfIn, lp<u32x2> l
 // DecCfg<FT>::ldsBytes(pb).  out.size(b) = capacity (bytes for raw ANS,
 // words for floats).  Pointer tables may ride in the first (InlineTable) argument
 // (BatchDesc::field).
-template <int FT, int KK, bool NT>
+// BAL: remaining-work wave priorities (single-generation grids).
+template <int FT, int KK, bool NT, bool BAL>
 __global__ __launch_bounds__(dec::kThreads) void k_decode(const InlineTable,
                                                           BatchDesc in, BatchDesc out,
                                                           uint32_t batchOffset, int pb,
@@ -560,7 +561,8 @@ __global__ __launch_bounds__(dec::kThreads) void k_decode(const InlineTable,
       }
       // full segments: unrolled, unmasked
       auto fullSeg = [&](int32_t g, const uint32_t (&cur)[K][R], uint32_t (&nxt)[K][R]) {
-        setPrioRemaining((chunksPerWG - 1 - pass) * uint32_t(nSeg) + uint32_t(g), chunksPerWG * uint32_t(nSeg));
+        if constexpr (BAL)
+          setPrioRemaining((chunksPerWG - 1 - pass) * uint32_t(nSeg) + uint32_t(g), chunksPerWG * uint32_t(nSeg));
         if (g > 0) loadRaw(g - 1, true, nxt);
 #pragma unroll
         for (int grp = int(dec::kSegSteps / dec::kUnroll) - 1; grp >= 0; --grp) {
