@@ -36,6 +36,9 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=200)
     p.add_argument("--warmup", type=int, default=20)
+    p.add_argument("--settle-ms", type=float, default=100.0,
+                   help="untimed back-to-back steps for this long after the warmup, before the timed "
+                        "region (GPU clocks ramp over tens of ms; recorded in the line as settle_ms)")
     p.add_argument("--workload", choices=("auto", "c2", "c5"), default="auto",
                    help="auto: c2 at N=1, c5 (fixed 8192-tensor batch, sharded) at N>1")
     p.add_argument("--batch", type=int, default=256, help="c2 tensors per GPU")
@@ -134,17 +137,36 @@ def main():
                 fam[k] = {"avg_ms": ms / launches, "launches": launches}
         return fam
 
-    # per-kernel breakdown: an extra profiled pass (event pair around every
-    # launch) outside the timed region; it also names the dominant kernel
+    # the dominant kernel family, from one profiled step (event pair around
+    # every launch); the full per-kernel breakdown is taken after the timed
+    # region so that the timed steps follow the settle phase directly
     C.profile_reset()
     C.profile_filter(None)
     C.profile(True)
-    for _ in range(max(args.warmup, 3)):
-        step()
+    step()
     torch.cuda.synchronize()
     C.profile(False)
-    breakdown = query_families()
-    dominant = max(breakdown, key=lambda k: breakdown[k]["avg_ms"]) if breakdown else None
+    probe = query_families()
+    dominant = max(probe, key=lambda k: probe[k]["avg_ms"]) if probe else None
+
+    # settle: untimed steps for a fixed wall time (clock ramp; no work of the
+    # timed region is skipped or cached by it).  The step count is fixed up
+    # front and agreed over ranks (every step of a rank > 1 has a collective)
+    t_s = time.perf_counter()
+    for _ in range(8):
+        step()
+    torch.cuda.synchronize()
+    per_step = (time.perf_counter() - t_s) / 8
+    settle_steps = max(0, int(args.settle_ms * 1e-3 / max(per_step, 1e-6)) - 8)
+    if world > 1:
+        c = torch.tensor([settle_steps], dtype=torch.int64, device=dev)
+        dist.all_reduce(c, op=dist.ReduceOp.MAX)
+        settle_steps = int(c.item())
+    for _ in range(settle_steps):
+        step()
+    torch.cuda.synchronize()
+    settle_steps += 8
+    settle_ms = (time.perf_counter() - t_s) * 1e3
 
     # timed region: barrier + sync on both sides, K steps, max over ranks; the
     # dominant kernel is timed live with hipEvents on its launch stream (only
@@ -164,6 +186,16 @@ def main():
     t1 = time.perf_counter()
     C.profile(False)
     C.profile_filter(None)
+    live = query_families()
+    # per-kernel breakdown of the other families: a profiled pass after the
+    # timed region
+    C.profile_reset()
+    C.profile(True)
+    for _ in range(max(args.warmup, 3)):
+        step()
+    torch.cuda.synchronize()
+    C.profile(False)
+    breakdown = query_families()
     elapsed = t1 - t0
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -176,7 +208,6 @@ def main():
         comp_total = comp_bytes
     ms_per_step = elapsed / args.steps * 1e3
     value = total * n * 2 * args.steps / elapsed / 1e9
-    live = query_families()
     fam = dict(breakdown)
     if dominant in live:
         fam[dominant] = live[dominant]  # the timed region's own measurement
@@ -198,6 +229,7 @@ def main():
     line = {
         "metric": METRIC, "value": round(value, 2), "unit": "GB/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
+        "settle_ms": round(settle_ms, 1), "settle_steps": settle_steps,
         "higher_is_better": True,
         "scaling": "strong" if workload == "c5" else "weak", "vs_baseline": None, "dtype": "u32",
         "data": "synthetic",

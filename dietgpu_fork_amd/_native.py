@@ -38,6 +38,8 @@ def _declare(L):
         "dietgpu_last_error": (ctypes.c_char_p, []),
         "dietgpu_device_error_count": (c_u32, [c_int]),
         "dietgpu_set_spin_cap": (None, [c_u32]),
+        "dietgpu_set_barrier_budget": (None, [c_u32]),
+        "dietgpu_test_occupy": (c_int, [P, c_u32, c_u32, c_u32]),
         "dietgpu_version": (ctypes.c_char_p, []),
         "dietgpu_stack_create": (vp, [c_int, P, c_size]),
         "dietgpu_stack_destroy": (None, [vp]),
@@ -80,7 +82,11 @@ def _declare(L):
         "dietgpu_profile_query": (c_int, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_double),
                                           ctypes.POINTER(ctypes.c_uint64)]),
     }
+    # test hooks absent from older builds (same-box A/B of earlier libraries)
+    optional = {"dietgpu_set_barrier_budget", "dietgpu_test_occupy"}
     for name, (res, args) in sig.items():
+        if name in optional and not hasattr(L, name):
+            continue
         f = getattr(L, name)
         f.restype = res
         f.argtypes = args

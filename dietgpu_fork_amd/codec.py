@@ -59,6 +59,13 @@ def set_spin_cap(polls):
     N.lib().dietgpu_set_spin_cap(int(polls))
 
 
+def set_barrier_budget(ticks):
+    """Test hook: 100 MHz ticks a single-pass compressor workgroup waits for
+    its team before counting the element itself (default 20000; 0 forces the
+    fallback on every team wait)."""
+    N.lib().dietgpu_set_barrier_budget(int(ticks))
+
+
 # ------------------------------------------------------------------ ANS ----
 
 def ans_encode_stride(data2d, prob_bits=10, checksum=False, ws=None, histogram=None,

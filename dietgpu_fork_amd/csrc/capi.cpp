@@ -15,6 +15,10 @@
 
 using namespace dietgpu;
 
+namespace dietgpu {
+void testOccupy(hipStream_t s, uint32_t micros, uint32_t workgroups, uint32_t ldsBytes);
+}
+
 struct dietgpu_stack {
   StackDeviceMemory* mem;
 };
@@ -303,6 +307,14 @@ uint32_t dietgpu_device_error_count(int reset) {
 }
 
 void dietgpu_set_spin_cap(uint32_t polls) { setSpinCap(polls); }
+void dietgpu_set_barrier_budget(uint32_t ticks) { setBarrierBudget(ticks); }
+
+int dietgpu_test_occupy(void* stream, uint32_t micros, uint32_t workgroups, uint32_t lds_bytes) {
+  return guarded([&] {
+    testOccupy(S(stream), micros, workgroups, lds_bytes);
+    return DIETGPU_OK;
+  });
+}
 
 void dietgpu_profile_enable(int on) { prof::setEnabled(on != 0); }
 void dietgpu_profile_filter(const char* kernel) { prof::setFilter(kernel); }

@@ -58,6 +58,20 @@ uint32_t residentSlots(const void* kernel, int threads, uint32_t dynLds) {
   return v;
 }
 
+uint32_t residentCUs() {
+  static std::mutex m;
+  static std::map<int, uint32_t> cache;
+  int dev = 0;
+  HIP_CHECK(hipGetDevice(&dev));
+  std::lock_guard<std::mutex> g(m);
+  auto it = cache.find(dev);
+  if (it != cache.end()) return it->second;
+  int cus = 0;
+  HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  cache[dev] = uint32_t(std::max(1, cus));
+  return cache[dev];
+}
+
 void checkProbBits(int pb) {
   DG_CHECK(pb >= 9 && pb <= 11, "unhandled pdf precision " << pb << " (must be 9, 10 or 11)");
 }
@@ -203,15 +217,22 @@ bool compressPersistent(StackDeviceMemory& res, int pb, bool useChecksum, uint32
   }
   const uint32_t grid = teamsPerRound * team;
 
-  auto part = res.alloc<uint32_t>(s, size_t(items) * kNumSymbols);
-  auto partCk = res.alloc<uint32_t>(s, kCk ? items : 1);
   auto slotMem = res.alloc<uint8_t>(s, size_t(grid) * pc::kBlocksPerItem * kSlotDataBytes);
   auto ck = res.alloc<uint32_t>(s, FT != 0 && useChecksum ? nb : 1);
   DeviceDescs dd(res, s, FT != 0 && useChecksum ? tabs : nullptr);  // k_checksum's view
-  // epoch-tagged flags in this stream's persistent arena: look-back flags,
-  // then team arrivals; the work-queue counter (no per-call zeroing)
-  const size_t flagBytes = roundUp64(uint64_t(items) * 8, 256);
-  SyncLease lease(res, s, flagBytes + size_t(items) * 4);
+  // epoch-tagged state in this stream's persistent arena (no per-call
+  // zeroing), one region per kind of word: the dequeue counters (at a fixed
+  // place: a call zeroes the next call's), the look-back flags, the tagged
+  // partial histograms then the tagged partial byte checksums, the per-team
+  // element log.  A team takes at most maxR rounds (pcompress.h, "Teams and
+  // elements"): twice the static share bounds the log while leaving the
+  // teams below it room for every element.
+  const size_t partBytes = size_t(items) * kNumSymbols * 4;
+  const uint32_t teams = grid / team;
+  const uint32_t maxR = 2 * divUp(nb, teams) + 2;
+  const size_t regions[kSyncRegions] = {16, size_t(items) * 8, partBytes + (kCk ? size_t(items) * 4 : 0),
+                                        size_t(teams) * maxR * 8};
+  SyncLease lease(res, s, regions);
   if (FT != 0 && useChecksum) {
     HIP_CHECK(hipMemsetAsync(ck.data(), 0, sizeof(uint32_t) * nb, s));
     // float checksum: the reference passes float-word counts as byte counts
@@ -225,10 +246,13 @@ bool compressPersistent(StackDeviceMemory& res, int pb, bool useChecksum, uint32
     }
   }
   PCompArgs a;
-  a.part = part.data();
-  a.partCk = partCk.data();
-  a.flags = reinterpret_cast<uint64_t*>(lease.base);
-  a.arrive = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(lease.base) + flagBytes);
+  a.ctr = static_cast<uint64_t*>(lease.base[kSyncCounters]);
+  a.flags = static_cast<uint64_t*>(lease.base[kSyncFlags]);
+  a.part = static_cast<uint32_t*>(lease.base[kSyncPartials]);
+  a.partCk = kCk ? a.part + size_t(items) * kNumSymbols : nullptr;
+  a.elog = static_cast<uint64_t*>(lease.base[kSyncLog]);
+  a.maxR = maxR;
+  a.slotSpan = std::max(1u, residentCUs());
   a.err = deviceErrorWord();
   a.slots = slotMem.data();
   a.teamStart = nullptr;
@@ -241,6 +265,7 @@ bool compressPersistent(StackDeviceMemory& res, int pb, bool useChecksum, uint32
   a.xcdTeams = xcdTeams ? 1u : 0u;
   a.epoch = lease.epoch;
   a.spinCap = spinCap();
+  a.fallbackTicks = barrierBudgetTicks();
   a.pb = pb;
   a.useChecksum = useChecksum;
   prof::Scope p("compress", s);

@@ -245,6 +245,90 @@ __device__ __forceinline__ uint32_t normalizeCount(uint32_t count, uint32_t tota
   return q;
 }
 
+// The same normalisation by ONE wave, lane l holding symbols 4l + j
+// (j < 4): no workgroup barrier, so the other waves of a workgroup can work
+// meanwhile.  c[j]: the counts in, the pdfs out; cdf[j]: the exclusive
+// cumulative pdfs (symbol order).  total > 0.  keysL, byRank: 256 words of
+// LDS each, private to this wave during the call.
+__device__ __forceinline__ void normalizeWave(uint32_t (&c)[4], uint32_t (&cdf)[4], uint32_t total, int pb,
+                                              uint32_t* keysL, uint32_t* byRank) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t W = 1u << pb;
+  uint32_t q[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float r = __fdiv_rn(float(c[j]), float(total));
+    q[j] = uint32_t(__fmul_rn(float(W), r));
+    if (c[j] > 0 && q[j] == 0) q[j] = 1;
+  }
+  const int diff = int(W) - int(waveSum(q[0] + q[1] + q[2] + q[3]));
+  if (diff > 0) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      q[j] += uint32_t(diff) / kNumSymbols + (4 * lane + j < uint32_t(diff) % kNumSymbols ? 1u : 0u);
+  } else if (diff < 0) {
+    // keys (q << 16) | s of the entries with q > 1 (the only ones ever
+    // decremented: a prefix [0, g) of the descending order), compacted into
+    // keysL; each one's rank = number of larger keys
+    uint32_t g0 = 0, key[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      key[j] = (q[j] << 16) | (4 * lane + j);
+      const uint64_t m = ballot(q[j] > 1);
+      if (q[j] > 1) keysL[g0 + mbcnt(m)] = key[j];
+      g0 += uint32_t(__popcll(m));
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    uint32_t rank[4] = {0, 0, 0, 0};
+    for (uint32_t t = 0; t < g0; ++t) {
+      const uint32_t k = keysL[t];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) rank[j] += k > key[j] ? 1u : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (q[j] > 1) byRank[rank[j]] = q[j];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    // the reference's rounds: each takes 1 from the k = min(d, g) lowest-
+    // ranked of the g entries still > 1 (entry r = lane + 64 i)
+    uint32_t Q[kNumSymbols / 64];
+#pragma unroll
+    for (uint32_t i = 0; i < kNumSymbols / 64; ++i) Q[i] = lane + 64 * i < g0 ? byRank[lane + 64 * i] : 1u;
+    int d = -diff;
+    while (d > 0) {
+      int g = 0;
+#pragma unroll
+      for (uint32_t i = 0; i < kNumSymbols / 64; ++i) g += __popcll(ballot(Q[i] > 1));
+      if (g == 0) break;  // reference asserts; unreachable for real tables
+      const int k = d < g ? d : g;
+#pragma unroll
+      for (uint32_t i = 0; i < kNumSymbols / 64; ++i) {
+        const int r = int(lane + 64 * i);
+        if (r >= g - k && r < g) Q[i] -= 1;
+      }
+      d -= k;
+    }
+#pragma unroll
+    for (uint32_t i = 0; i < kNumSymbols / 64; ++i)
+      if (lane + 64 * i < g0) byRank[lane + 64 * i] = Q[i];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (q[j] > 1) q[j] = byRank[rank[j]];
+  }
+  const uint32_t lsum = q[0] + q[1] + q[2] + q[3];
+  const uint32_t base = waveInclusiveScan(lsum) - lsum;
+  cdf[0] = base;
+  cdf[1] = base + q[0];
+  cdf[2] = cdf[1] + q[1];
+  cdf[3] = cdf[2] + q[2];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) c[j] = q[j];
+}
+
 // Encode table entry (internal, never archived) of a symbol with pdf q and
 // cumulative frequency cdf:
 //   x = pdf << (31 - pb)              renormalisation threshold

@@ -1,7 +1,10 @@
-// Cross-workgroup hand-off helpers shared by the persistent compressor
-// (pcompress.h) and the fused sparse compaction (sparse.hip): sc1 (agent-scope
-// relaxed) loads / stores, and a decoupled look-back over epoch-tagged,
-// poison-carrying 8 B flags (MI355X_MICROARCH.md sc1 hand-off, row 1).
+// Cross-workgroup hand-off helpers of the persistent compressor
+// (pcompress.h): sc1 (agent-scope relaxed) loads / stores, and a decoupled
+// look-back over epoch-tagged, poison-carrying 8 B flags (MI355X_MICROARCH.md
+// sc1 hand-off, row 1).  encode.h's lookBack (the three-kernel k_encode, whose
+// flags are zeroed per call by k_normalize instead of epoch-tagged) uses the
+// same bit layout -- status in bits 63:62, poison in bit 61 (kFlagPoisonE ==
+// kFlagPoison), value in bits 31:0 -- so the two stay interchangeable.
 #pragma once
 
 #include "encode.h"
@@ -10,6 +13,7 @@
 namespace dietgpu {
 
 constexpr uint64_t kFlagPoison = 1ull << 61;
+static_assert(kFlagPoison == kFlagPoisonE, "one poison bit for both look-backs");
 
 __device__ __forceinline__ uint32_t ldSc1(gp<const uint32_t> p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -20,7 +24,7 @@ __device__ __forceinline__ void stSc1(gp<uint32_t> p, uint32_t v) {
 
 // Decoupled look-back (encode.h lookBack) over earlier members [0, x) with
 // epoch-tagged, poison-carrying flags: bits 63:62 status (1 aggregate, 2
-// inclusive prefix), 61 poison, 60:32 epoch, 31:0 value.  A flag of another
+// inclusive prefix), 61 poison, 47:32 epoch, 31:0 value.  A flag of another
 // epoch reads as "not yet published".  Whole wave; returns the sum of the
 // values of members [0, x); `poison` in: this member's own, out: whether any
 // member [0, x] is poisoned (or the wait ran out of polls).

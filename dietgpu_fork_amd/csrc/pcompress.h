@@ -15,9 +15,10 @@
 // the items are dealt out in rounds of one grid: workgroup w takes item
 // r * grid + j(w) in round r.  j(w) keeps each team on one XCD (workgroups
 // w, w + 8, ... share one under the observed round-robin placement), so the
-// team's hand-offs stay in one L2 (speed only, never correctness).  No
-// atomics hand out work: a shared work-queue counter serialises at ~90
-// dequeues per microsecond, 11 us per round of 1024 workgroups.
+// team's hand-offs stay in one L2 (speed only, never correctness), and gives
+// the members of a team increasing workgroup indices.  No atomics hand out
+// work: a shared work-queue counter serialises at ~90 dequeues per
+// microsecond, 11 us per round of 1024 workgroups.
 //
 // Pipeline.  A workgroup holds two items: E, whose table is known and which it
 // encodes, and L (its next round's item), which it loads.  Per iteration,
@@ -26,27 +27,33 @@
 // segments ahead, raw float bytes straight to the archive, ANS symbols
 // transposed into the registers E's segment just freed, counted in an LDS
 // histogram), so the HBM stream of L overlaps the VALU-bound encode of E
-// inside every wave.  Then it publishes L's partial histogram, places E
-// (decoupled look-back, headers, payload copy from the LDS rings), waits at
-// L's team barrier and normalises L (every member sums the team's partials
-// itself: one hop).
-
-// Cross-workgroup hand-offs follow MI355X_MICROARCH.md's sc1 protocol (row 1
-// of its hand-off table): payloads are stored with agent-scope relaxed (sc1)
-// stores, every storing wave waits vmcnt(0), a workgroup barrier, then one
-// lane signals; consumers poll with sc1 loads and read the payload with sc1
-// loads only.
+// inside every wave.  The hand-off window then publishes L's partial
+// histogram and E's look-back aggregate, loads the team's partials of L while
+// wave 0 runs E's look-back, and after one workgroup barrier wave 0
+// normalises L (every member sums the team's partials itself: one hop) while
+// waves 1-3 copy E's payload out of the LDS rings.
 //
-// Forward progress.  Waits are on the team barrier of L (all members loaded)
-// and on the look-back of E (lower members placed).  A team's items all
-// belong to one round, and a workgroup reaches round r's barrier only after
-// publishing every earlier round's item, so (by induction over rounds) every
-// wait ends once the grid is resident: the host launches at most the
-// occupancy-reported number of workgroups.  Each wait is bounded by a poll
-// cap (a kernel argument); a wait that runs out POISONS the element instead
+// Cross-workgroup hand-offs follow MI355X_MICROARCH.md's tagged-granule form:
+// a partial histogram word is {epoch << 16 | count} written by one sc1 store
+// and read with sc1 loads, so its consumer needs no arrival flag (no drain of
+// the producer's stores, no barrier, one memory round trip per hop); the
+// look-back flags carry their value and epoch in one 8 B word.
+//
+// Forward progress does not depend on the grid being co-resident.  The only
+// wait on workgroups that may not have been dispatched is L's team barrier
+// (its members have higher as well as lower indices); it is bounded by a time
+// budget (PCompArgs::fallbackTicks), after which the workgroup counts L's
+// element itself from the input (an extra read on this slow path only) and
+// goes on.  Every other wait is the look-back on LOWER members of E's team,
+// i.e. lower workgroup indices of the same round, dispatched before this one
+// (in-order dispatch) and, by induction over rounds and member index, never
+// waiting on a workgroup that is not resident.  Another kernel holding CUs
+// (a second compress on another stream, an RCCL collective) therefore delays
+// the call but cannot stall it.  The look-back is still bounded by a poll cap
+// (a kernel argument); a look-back that runs out POISONS the element instead
 // of guessing: the poison bit rides in the look-back flag to the element's
 // last member, which writes outSize = 0 and counts the element in the device
-// error word.
+// error word (a poisoned element's output bytes are undefined).
 #pragma once
 
 #include <utility>
@@ -80,9 +87,8 @@ constexpr uint32_t kHistWords = 256 * kHistStride;
 }  // namespace pc
 
 struct PCompArgs {
-  uint32_t* part;        // [items][256] partial histograms (sc1)
-  uint32_t* partCk;      // [items] partial byte checksums (FT 0 with checksum)
-  uint32_t* arrive;      // [items] team arrival flags = epoch (sync arena)
+  uint32_t* part;        // [items][256] partial histograms, epoch << 16 | count (sync arena)
+  uint32_t* partCk;      // [items] partial byte checksums, epoch << 16 | xor (FT 0 with checksum)
   uint64_t* flags;       // [items] look-back flags (sync arena)
   uint32_t* err;         // device error word (elements poisoned)
   uint8_t* slots;        // [grid][8][kSlotDataBytes] spill space of each workgroup
@@ -94,8 +100,13 @@ struct PCompArgs {
   uint32_t nb;
   uint32_t grid;         // workgroups = items per round (a whole number of teams)
   uint32_t xcdTeams;     // 1: team members share w % 8 (teams per round % 8 == 0)
+  uint64_t* ctr;         // [2] element dequeue counters, this call's at epoch & 1 (sync arena)
+  uint64_t* elog;        // [teams][maxR] element of each team's round, epoch << 32 | element (sync arena)
+  uint32_t maxR;         // rounds a team may take
+  uint32_t slotSpan;     // workgroups per dispatch slot (the CU count): slot = blockIdx / slotSpan
   uint32_t epoch;
-  uint32_t spinCap;      // polls per wait before poisoning
+  uint32_t spinCap;      // polls per look-back before poisoning
+  uint32_t fallbackTicks;  // team-barrier wait (100 MHz ticks) before counting the element itself
   int pb;
   bool useChecksum;
 };
@@ -166,9 +177,17 @@ __device__ __forceinline__ T kernArg(size_t off) {
 #endif
 }
 
+__device__ __forceinline__ uint64_t realtime() {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_s_memrealtime();  // 100 MHz
+#else
+  return 0;
+#endif
+}
+
 // Grid: one generation of resident workgroups (1-D), 256 threads.  Pointer
 // tables may ride in the first (InlineTable) argument (BatchDesc::inl).  4
-// waves per SIMD (<= 128 VGPRs, ~36 KB of LDS per workgroup).
+// waves per SIMD (<= 128 VGPRs, ~40 KB of LDS per workgroup).
 template <int FT, bool kCk>
 __global__ __launch_bounds__(pc::kThreads) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_pcompress(
     const InlineTable, BatchDesc, BatchDesc, PCompArgs) {
@@ -190,18 +209,37 @@ __global__ __launch_bounds__(pc::kThreads) __attribute__((amdgpu_waves_per_eu(4,
   __shared__ __attribute__((aligned(16))) uint32_t tblS[kNumSymbols * 4];
   __shared__ __attribute__((aligned(16))) uint8_t symT[pc::kBlocksPerItem][pc::kSegWords];
   __shared__ uint32_t trashS[pc::kWaves][64];
-  __shared__ uint32_t keys[kNumSymbols];
-  __shared__ uint16_t pdfS[kNumSymbols];
+  __shared__ __attribute__((aligned(16))) uint32_t keys[kNumSymbols];
+  __shared__ __attribute__((aligned(16))) uint16_t pdfS[kNumSymbols];
   __shared__ uint32_t red[pc::kWaves];
+  __shared__ uint32_t ckS[pc::kWaves];
   __shared__ uint32_t cwE[pc::kBlocksPerItem], flE[pc::kBlocksPerItem], preE[pc::kBlocksPerItem];
-  __shared__ uint32_t stateS;
+  __shared__ uint32_t poisonS, sigS;
 
   const uint32_t tid = threadIdx.x;
-  const uint32_t w = readfirst(tid >> 6), lane = tid & 63, h = lane >> 5, l = lane & 31;
-  uint32_t hv = h ? ~0u : 0u;
+  // the lane's half (0: lanes 0-31, 1: lanes 32-63), recomputed at each use
+  // by three VALU instructions: held live across the pipeline it spills, and
+  // a reload's vmcnt wait drains the input loads in flight
+  auto halfNow = []() __attribute__((always_inline)) -> uint32_t {
+    uint32_t hh;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0\n\tv_lshrrev_b32 %0, 5, %0"
+                 : "=v"(hh));
+    return hh;
+  };
+  const uint32_t w = readfirst(tid >> 6), lane = tid & 63, l = lane & 31;
+  // lane / thread index recomputed at each use (the hand-off code's LDS and
+  // global addresses derive from them: hoisted to the kernel entry they are
+  // spilled, and each scratch reload is a memory round trip -- microseconds
+  // while the other workgroups stream)
+  auto laneNow = []() __attribute__((always_inline)) -> uint32_t {
+    uint32_t v;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(v));
+    return v;
+  };
+  auto tidNow = [&]() __attribute__((always_inline)) -> uint32_t { return (w << 6) + laneNow(); };
+  uint32_t hv = halfNow() ? ~0u : 0u;
   asm volatile("" : "+v"(hv));  // keep `hv & x` a v_and
   const uint32_t trashAddr = uint32_t(size_t((lp<uint32_t>)&trashS[w][lane]));
-  lp<uint8_t> myT = (lp<uint8_t>)&symT[2 * w + h][0];
   lp<uint32_t> hcol = (lp<uint32_t>)&hist[l & (pc::kHistCols - 1)];
   // quad byte transpose of the symbols (phase 1): lane l = 4 qm + qr
   const uint32_t qr = l & 3, qm = l >> 2;
@@ -212,6 +250,7 @@ __global__ __launch_bounds__(pc::kThreads) __attribute__((amdgpu_waves_per_eu(4,
 
   for (uint32_t i = tid; i < pc::kHistWords / 4; i += pc::kThreads)
     *(lp<u32x4>)&hist[4 * i] = u32x4{0, 0, 0, 0};
+  if (tid == 0) sigS = 0;
   static_assert(pc::kHistWords % 4 == 0, "16 B zeroing");
   static_assert(pc::kSpill + 32 * enc::kUnroll <= pc::kRing, "ring overflow between spill checks");
 
@@ -223,58 +262,124 @@ __global__ __launch_bounds__(pc::kThreads) __attribute__((amdgpu_waves_per_eu(4,
   static_assert(sizeof(WordT) <= 4, "single-segment formats have words of at most 4 bytes");
   uint32_t ck = 0;
 
-  // this workgroup's item of round r (>= items: none)
-  auto itemAt = [&](uint32_t r) __attribute__((always_inline)) -> uint32_t {
+  // Teams and elements.  Team T (members x = 0 .. team-1, increasing
+  // workgroup indices) takes element T in round 0 and teams + T in round 1;
+  // later rounds' elements come from a dequeue counter, taken by member 0 two
+  // rounds ahead and logged per team (elog[T][r]), so teams that run ahead
+  // take more elements (the SIMD arbiter favours the earlier-dispatched
+  // workgroups of a CU: with a static deal their teams finished rounds of
+  // work ahead of the last ones).
+  auto teamX = [&](uint32_t& T, uint32_t& X) __attribute__((always_inline)) {
     const PCompArgs ka = A();
-    uint32_t j = blockIdx.x;
-    if (ka.xcdTeams) {  // w = xcd + 8 (group * team + x), team slot = group * 8 + xcd
+    if (ka.xcdTeams) {  // w = xcd + 8 (group * team + x), team T = group * 8 + xcd
       const uint32_t xcd = blockIdx.x & 7u, q = blockIdx.x >> 3;
-      const uint32_t grp = q / ka.team, x = q - grp * ka.team;
-      j = (grp * 8 + xcd) * ka.team + x;
+      const uint32_t grp = q / ka.team;
+      X = q - grp * ka.team;
+      T = grp * 8 + xcd;
+    } else {
+      T = blockIdx.x / ka.team;
+      X = blockIdx.x - T * ka.team;
     }
-    const uint64_t i = uint64_t(r) * ka.grid + j;
-    return i < ka.items ? uint32_t(i) : ka.items;
+  };
+  // item of element e (>= nb: none) for this member
+  auto itemOfElem = [&](uint32_t e) __attribute__((always_inline)) -> uint32_t {
+    uint32_t T, X;
+    teamX(T, X);
+    const PCompArgs ka = A();
+    return e < ka.nb ? e * ka.team + X : ka.items;
+  };
+  // element of this team's round r (r >= 2: from the log, written by member
+  // 0 a round earlier; a lower workgroup index, so the wait always ends)
+  auto elemOfRound = [&](uint32_t r) __attribute__((always_inline)) -> uint32_t {
+    uint32_t T, X;
+    teamX(T, X);
+    const PCompArgs ka = A();
+    const uint32_t teams = ka.grid / ka.team;
+    if (r < 2) return min(r * teams + T, ka.nb);
+    if (r >= ka.maxR) return ka.nb;
+    gp<const uint64_t> slot = G(ka.elog) + uint64_t(T) * ka.maxR + r;
+    uint64_t v = 0;
+    // (not bounded by spinCap: no element's archive depends on this wait,
+    // whose writer is never blocked; the bound only guards logic errors)
+    for (uint32_t spins = 0; spins < (1u << 26); ++spins) {
+      v = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (uint32_t(v >> 32) == ka.epoch) return min(uint32_t(v), ka.nb);
+      __builtin_amdgcn_s_sleep(2);
+    }
+    // (unreachable: member 0 never waits unboundedly) count it as abandoned
+    __hip_atomic_fetch_add(G(ka.err), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return ka.nb;
+  };
+  // member 0: take the element of round r (>= 2) and log it
+  auto dequeueRound = [&](uint32_t r) __attribute__((always_inline)) {
+    uint32_t T, X;
+    teamX(T, X);
+    const PCompArgs ka = A();
+    if (X != 0 || r >= ka.maxR) return;
+    const uint32_t teams = ka.grid / ka.team;
+    const uint64_t tag = uint64_t(ka.epoch) << 32;
+    // one returning add on this call's counter (zeroed by the previous call
+    // on this stream, see below): a compare-and-swap loop under 64
+    // contenders took 17 us
+    const uint32_t e = 2 * teams + uint32_t(__hip_atomic_fetch_add(G(ka.ctr) + (ka.epoch & 1u), 1ull,
+                                                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    __hip_atomic_store(G(ka.elog) + uint64_t(T) * ka.maxR + r, tag | min(e, ka.nb), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
   };
   auto pairSize = [&](const PItem& it, int hh) __attribute__((always_inline)) -> uint32_t {
     const uint32_t bk = it.x * pc::kBlocksPerItem + 2 * w + hh;
     return bk < it.nBlocks ? min(kBlockSize, it.n - bk * kBlockSize) : 0u;
   };
+  // this lane's block size of an item (h ? pairSize(it, 1) : pairSize(it, 0))
+  auto laneSize = [&](const PItem& it) __attribute__((always_inline)) -> uint32_t {
+    const uint32_t bk = it.x * pc::kBlocksPerItem + 2 * w + halfNow();
+    return bk < it.nBlocks ? min(kBlockSize, it.n - bk * kBlockSize) : 0u;
+  };
   auto srcOf = [&](const PItem& it) __attribute__((always_inline)) -> gp<const WordT> {
+    const uint32_t hh = halfNow();
     return (gp<const WordT>)startOf(IN(), it.b) +
-           uint64_t(it.x * pc::kBlocksPerItem + 2 * w + h) * kBlockSize;
+           uint64_t(it.x * pc::kBlocksPerItem + 2 * w + hh) * kBlockSize;
   };
 
-  // 16 B streaming loads of segment g of this lane's block (the input is read
-  // once; non-temporal, so the caches keep the archives for the decoder:
-  // c2 step 267 -> 239 us together with the decoder's streaming stores,
-  // same-box A/B), issued unconditionally (an
+  // 16 B streaming loads of segment g of this lane's block into load slot
+  // g % D (the input is read once; non-temporal, so the caches keep the
+  // archives for the decoder: c2 step 267 -> 239 us together with the
+  // decoder's streaming stores, same-box A/B), issued unconditionally (an
   // item's load schedule is then branch-free, so the compiler's wait counts
   // stay exact instead of draining every load in flight at a branch merge):
-  // a vector with no word of the block reads the element's first vector
-  // instead.  16 B-aligned input only (the host sends anything else down the
-  // three-kernel path): a vector holding the last valid word is then a whole
-  // 16 B chunk of the same page.
-  auto load = [&](gp<const WordT> elem, gp<const WordT> src, uint32_t uw, uint32_t g)
+  // a vector with no word of the block (or of no item at all) reads a dummy
+  // vector of this workgroup's slot space instead.  16 B-aligned input only
+  // (the host sends anything else down the three-kernel path): a vector
+  // holding the last valid word is then a whole 16 B chunk of the same page.
+  auto load = [&](gp<const WordT> dummy, gp<const WordT> src, uint32_t uw, uint32_t g)
                   __attribute__((always_inline)) {
+    // (opaque lane: the per-segment offsets are recomputed here, never
+    // hoisted out of the loop -- 16 of them held live spill to scratch)
+    uint32_t ll = l;
+    asm volatile("" : "+v"(ll));
 #pragma unroll
     for (int k = 0; k < V; ++k) {
-      const uint32_t j0 = g * pc::kSegWords + (k * 32 + l) * kWPV;
-      pv[g % D][k] = ld16nt(j0 < uw ? src + j0 : elem);
+      const uint32_t j0 = g * pc::kSegWords + (k * 32 + ll) * kWPV;
+      pv[g % D][k] = ld16nt(j0 < uw ? src + j0 : dummy);
     }
   };
 
-  // ---- phase-1 pieces for segment g of item L ----
-  // split: raw bytes -> archive, symbols -> myT.  kFull: both blocks of the
-  // pair whole; otherwise words at or past the block's end are zeroed (their
-  // raw bytes are the archive's zero padding, their symbols are never
-  // counted or encoded) and vectors wholly past it store nothing.
+  // ---- split segment g of an item from load slot g % D: raw bytes ->
+  // archive, symbols -> this half-wave's symbol buffer.  kFull: both blocks of the pair
+  // whole; otherwise words at or past the block's end are zeroed (their raw
+  // bytes are the archive's zero padding, their symbols are never counted or
+  // encoded) and vectors wholly past it store nothing.
   auto split = [&](const PItem& it, gp<uint8_t> raw, uint32_t uw, uint32_t g, auto fullTag)
                    __attribute__((always_inline)) {
     constexpr bool kFull = decltype(fullTag)::value;
-    const uint32_t blk = it.x * pc::kBlocksPerItem + 2 * w + h;
+    const uint32_t hh = halfNow();
+    const uint32_t blk = it.x * pc::kBlocksPerItem + 2 * w + hh;
+    lp<uint8_t> myT = (lp<uint8_t>)&symT[2 * w + hh][0];
+    uint32_t ll = l;
+    asm volatile("" : "+v"(ll));
 #pragma unroll
     for (int k = 0; k < V; ++k) {
-      const uint32_t off = (k * 32 + l) * kWPV;  // word offset in the segment
+      const uint32_t off = (k * 32 + ll) * kWPV;  // word offset in the segment
       const uint32_t j0 = g * pc::kSegWords + off;
       const uint32_t i0 = blk * kBlockSize + j0;
       uint4 v = pv[g % D][k];
@@ -294,11 +399,13 @@ __global__ __launch_bounds__(pc::kThreads) __attribute__((amdgpu_waves_per_eu(4,
       if constexpr (kCk) ck ^= v.x ^ v.y ^ v.z ^ v.w;
     }
   };
-  // transpose: lane l = 4m + r reads the dwords of rows 4q + r (q < 4),
-  // columns 4m..4m+3; a 4 x 4 byte transpose inside its quad (two DPP
-  // exchanges + v_perm) leaves it column l, steps 4q..4q+3, packed for the
-  // encoder: 4 ds_read_b32 instead of 16 ds_read_u8.  Then count.
+  // transpose segment g from the symbol buffer: lane l = 4m + r reads the
+  // dwords of rows 4q + r (q < 4), columns 4m..4m+3; a 4 x 4 byte transpose
+  // inside its quad (two DPP exchanges + v_perm) leaves it column l, steps
+  // 4q..4q+3, packed for the encoder: 4 ds_read_b32 instead of 16
+  // ds_read_u8.  Then count.
   auto transposeCount = [&](uint32_t g, uint32_t uw, bool masked) __attribute__((always_inline)) {
+    lp<const uint8_t> myT = (lp<const uint8_t>)&symT[2 * w + halfNow()][0];
     uint32_t W[4];
 #pragma unroll
     for (uint32_t q = 0; q < 4; ++q) W[q] = *(lp<const uint32_t>)(myT + (4 * q + qr) * 32 + 4 * qm);
@@ -379,109 +486,105 @@ __global__ __launch_bounds__(pc::kThreads) __attribute__((amdgpu_waves_per_eu(4,
     }
   };
 
-  // ---- publish L's partial histogram, arrive ----
-  // (after a workgroup barrier: every wave's counts are in)
-  auto publish = [&](const PItem& it) __attribute__((always_inline)) {
+  // ---- publish L's partial histogram (and byte checksum): one tagged word
+  // per bin, epoch << 16 | count (an item counts at most 32768 symbols) ----
+  // (after a workgroup barrier: every wave's counts and ckS are in).  The
+  // data carries its own epoch, so the consumer needs no separate arrival
+  // flag: no drain of the stores, no barrier, one memory round trip per hop
+  // (MI355X_MICROARCH.md: a tagged granule written by one sc1 store).  The
+  // words live in the persistent epoch-tagged sync arena, never in scratch a
+  // stale value could come from.
+  auto publishHist = [&](const PItem& it) __attribute__((always_inline)) {
+    const uint32_t tid = tidNow(), lane = laneNow();
+    (void)tid;
+    (void)lane;
     uint32_t cnt = 0;
 #pragma unroll
     for (uint32_t k = 0; k < pc::kHistCols; ++k) {
       cnt += hist[tid * pc::kHistStride + k];
       hist[tid * pc::kHistStride + k] = 0;
     }
-    stSc1(G(A().part) + uint64_t(it.i) * kNumSymbols + tid, cnt);
+    const uint32_t tag = A().epoch << 16;
+    stSc1(G(A().part) + uint64_t(it.i) * kNumSymbols + tid, tag | cnt);
     if constexpr (kCk) {
-      uint32_t c = (ck ^ (ck >> 8) ^ (ck >> 16) ^ (ck >> 24)) & 0xffu;
-      c = waveXor(c);
-      if (lane == 0) red[w] = c;
-      __syncthreads();
-      if (tid == 0) stSc1(G(A().partCk) + it.i, red[0] ^ red[1] ^ red[2] ^ red[3]);
-      ck = 0;
+      if (tid == 0) stSc1(G(A().partCk) + it.i, tag | (ckS[0] ^ ckS[1] ^ ckS[2] ^ ckS[3]));
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0) stSc1(G(A().arrive) + it.i, A().epoch);
   };
 
-  // ---- team barrier + normalisation of L: table in tblS, pdf in pdfS ----
-  // Returns (uniform) whether the wait ran out of polls; ckOut: the element's
-  // byte checksum (kCk).
-  auto barrierNormalize = [&](const PItem& it, uint32_t& ckOut) __attribute__((always_inline)) -> bool {
-    if (w == 0) {
-      bool ok = it.team == 1;  // a team of one waits for nobody
-      for (uint32_t spins = 0; !ok && spins < A().spinCap; ++spins) {
-        const bool inT = lane >= it.team || ldSc1(G(A().arrive) + it.tb + lane) == A().epoch;
-        if (ballot(!inT) == 0) {
-          ok = true;
-          break;
+  // ---- slow path: L's element counted by this workgroup from its input ----
+  // (the team did not complete within the budget).  Returns this thread's
+  // bin count; ckOut: the element's byte checksum (kCk).  hist is zero on
+  // entry and on exit.
+  auto countElement = [&](const PItem& it, uint32_t& ckOut) __attribute__((always_inline)) -> uint32_t {
+    const uint32_t tid = tidNow(), lane = laneNow();
+    (void)tid;
+    (void)lane;
+    const gp<const WordT> src = (gp<const WordT>)startOf(IN(), it.b);
+    const uint32_t nv = divUp(it.n, kWPV);
+    uint32_t c = 0;
+    for (uint32_t v = tid; v < nv; v += pc::kThreads) {
+      const uint4 x = ld16(src + uint64_t(v) * kWPV);
+      const WordT* ws = reinterpret_cast<const WordT*>(&x);
+#pragma unroll
+      for (uint32_t k = 0; k < kWPV; ++k) {
+        if (v * kWPV + k < it.n) {
+          __hip_atomic_fetch_add(hcol + __umul24(compOf<FT>(ws[k], 0), pc::kHistStride), 1u, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_WORKGROUP);
+          if constexpr (kCk) c ^= uint32_t(ws[k]);
         }
-        __builtin_amdgcn_s_sleep(1);
       }
-      if (lane == 0) stateS = ok ? 0u : 1u;
     }
-    __syncthreads();
-    const bool timedOut = readfirst(stateS) != 0;
-    gp<const uint32_t> hp = G(A().part) + uint64_t(it.tb) * kNumSymbols + tid;
-    // (16 loads in flight at a time: L's symbols hold 32 VGPRs meanwhile)
-    uint32_t count = 0;
-    for (uint32_t k0 = 0; k0 < it.team; k0 += 16) {
-      uint32_t acc[16];
-#pragma unroll
-      for (uint32_t k = 0; k < 16; ++k)
-        acc[k] = k0 + k < it.team ? ldSc1(hp + uint64_t(k0 + k) * kNumSymbols) : 0u;
-#pragma unroll
-      for (uint32_t k = 0; k < 16; ++k) count += acc[k];
-    }
-    const uint32_t q = it.n == 0 ? 0u : normalizeCount(count, it.n, A().pb, keys, red);
     if constexpr (kCk) {
-      uint32_t c = tid < it.team ? ldSc1(G(A().partCk) + it.tb + tid) : 0u;
       c = waveXor(c);
-      __syncthreads();
       if (lane == 0) red[w] = c;
-      __syncthreads();
-      ckOut = red[0] ^ red[1] ^ red[2] ^ red[3];
     }
-    const uint32_t cdf = blockExclusiveScan<pc::kThreads>(q, red, nullptr);
-    const uint4 e = encTableEntryReg(q, cdf, A().pb);
-    *(lp<u32x4>)&tblS[4 * tid] = u32x4{e.x, e.y, e.z, e.w};
-    pdfS[tid] = uint16_t(q);
     __syncthreads();
-    return timedOut;
+    uint32_t cnt = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < pc::kHistCols; ++k) {
+      cnt += hist[tid * pc::kHistStride + k];
+      hist[tid * pc::kHistStride + k] = 0;
+    }
+    if constexpr (kCk) ckOut = red[0] ^ red[1] ^ red[2] ^ red[3];
+    __syncthreads();
+    return cnt;
   };
 
   // ---- E's aggregate (its words, rounded to 8 per block) -> its look-back flag ----
-  auto publishAgg = [&](const PItem& it, bool poison) __attribute__((always_inline)) {
+  auto publishAgg = [&](const PItem& it) __attribute__((always_inline)) {
+    const uint32_t tid = tidNow(), lane = laneNow();
+    (void)tid;
+    (void)lane;
     const uint32_t first = it.x * pc::kBlocksPerItem;
     const uint32_t nk = first < it.nBlocks ? min(pc::kBlocksPerItem, it.nBlocks - first) : 0u;
     const uint32_t r = lane < nk ? roundUp(cwE[lane], 8) : 0u;
     const uint32_t agg = readfirst(__shfl(waveInclusiveScan(r), 63));
     if (lane == 0)
       __hip_atomic_store(G(A().flags) + it.tb + it.x,
-                         (it.x == 0 ? kFlagPrefix : kFlagAgg) | (poison ? kFlagPoison : 0ull) |
-                             (uint64_t(A().epoch) << 32) | agg,
+                         (it.x == 0 ? kFlagPrefix : kFlagAgg) | (uint64_t(A().epoch) << 32) | agg,
                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   };
 
-  // ---- placement of E: look-back, headers, payload copy-out ----
-  auto place = [&](const PItem& it, bool poison, uint32_t ckE) __attribute__((always_inline)) {
-    // spilled words are read back by other waves of this workgroup: a wave
-    // that spilled waits for its stores (the others need not drain the
-    // raw-section stores of the split)
-    if (p.flushed[0] | p.flushed[1]) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+  // ---- wave 0: E's look-back -> preE, the last member's header total ----
+  auto lookBackE = [&](const PItem& it) __attribute__((always_inline)) {
+    const uint32_t tid = tidNow(), lane = laneNow();
+    (void)tid;
+    (void)lane;
     const uint32_t first = it.x * pc::kBlocksPerItem;
     const uint32_t nk = first < it.nBlocks ? min(pc::kBlocksPerItem, it.nBlocks - first) : 0u;
     gp<uint8_t> base = startOf(OUT(), it.b);
     gp<uint8_t> o = base + (FT == 0 ? 0u : 32u + floatRawBytes(FT, it.n));  // ANS archive
     gp<uint8_t> states = o + kANSHeaderBytes + kPdfBytes;
     gp<uint2> bwords = (gp<uint2>)(states + uint64_t(kStateBytesPerBlock) * it.nBlocks);
-    if (w == 0) {
-      const uint32_t r = lane < nk ? roundUp(cwE[lane], 8) : 0u;
-      const uint32_t inc = waveInclusiveScan(r);
-      const uint32_t agg = readfirst(__shfl(inc, 63));
-      bool pz = poison;
-      const uint32_t excl = lookBackPoison(G(A().flags) + it.tb, it.x, agg, A().epoch, A().spinCap, pz, false);
-      if (lane < nk) preE[lane] = excl + inc - r;
-      if (lane == 0 && it.x == it.team - 1) {
+    const uint32_t r = lane < nk ? roundUp(cwE[lane], 8) : 0u;
+    const uint32_t inc = waveInclusiveScan(r);
+    const uint32_t agg = readfirst(__shfl(inc, 63));
+    bool pz = false;
+    const uint32_t excl = lookBackPoison(G(A().flags) + it.tb, it.x, agg, A().epoch, A().spinCap, pz, false);
+    if (lane < nk) preE[lane] = excl + inc - r;
+    if (lane == 0) {
+      poisonS = pz ? 1u : 0u;
+      if (it.x == it.team - 1) {
         if (pz) {
           if (A().outSize) G(A().outSize)[it.b] = 0u;
           __hip_atomic_fetch_add(G(A().err), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -491,56 +594,84 @@ __global__ __launch_bounds__(pc::kThreads) __attribute__((amdgpu_waves_per_eu(4,
         }
       }
     }
-    if (it.x == 0) {
-      // header fields known before encoding, the pdf table, raw-section tails
-      if (tid == 0) {
-        const bool ansCk = FT == 0 && A().useChecksum;
-        const uint32_t ckv = FT == 0 ? ckE : (A().ckIn ? G(A().ckIn)[it.b] : 0u);
-        gp<uint32_t> hdr = (gp<uint32_t>)o;
-        hdr[0] = kANSMagicVersion;
-        hdr[1] = it.nBlocks;
-        hdr[2] = it.n;
-        hdr[4] = uint32_t(A().pb) | (ansCk ? 0x10u : 0u);
-        hdr[5] = ansCk ? ckv : 0u;
-        hdr[6] = 0;
-        hdr[7] = 0;
-        if constexpr (FT != 0) {
-          gp<uint32_t> fh = (gp<uint32_t>)base;
-          fh[0] = kFloatMagicVersion;
-          fh[1] = it.n;
-          fh[2] = uint32_t(FT) | (A().useChecksum ? 0x10u : 0u);
-          fh[3] = A().useChecksum ? ckv : 0u;
-          fh[5] = 0;
-          fh[6] = 0;
-          fh[7] = 0;
-        }
-      }
-      ((gp<uint16_t>)(o + kANSHeaderBytes))[tid] = pdfS[tid];
+  };
+
+  // ---- wave 0, after L's normalisation: L's header fields known before
+  // encoding (all but the word totals), its pdf table and the raw section's
+  // rounding tails, by the team's first member ----
+  auto writeHeadFixedL = [&](const PItem& it, uint32_t ckv) __attribute__((always_inline)) {
+    const uint32_t tid = tidNow(), lane = laneNow();
+    (void)tid;
+    (void)lane;
+    gp<uint8_t> base = startOf(OUT(), it.b);
+    gp<uint8_t> o = base + (FT == 0 ? 0u : 32u + floatRawBytes(FT, it.n));  // ANS archive
+    if (lane == 0) {
+      const bool ansCk = FT == 0 && A().useChecksum;
+      if (FT != 0) ckv = A().ckIn ? G(A().ckIn)[it.b] : 0u;
+      gp<uint32_t> hdr = (gp<uint32_t>)o;
+      hdr[0] = kANSMagicVersion;
+      hdr[1] = it.nBlocks;
+      hdr[2] = it.n;
+      hdr[4] = uint32_t(A().pb) | (ansCk ? 0x10u : 0u);
+      hdr[5] = ansCk ? ckv : 0u;
+      hdr[6] = 0;
+      hdr[7] = 0;
       if constexpr (FT != 0) {
-        gp<uint8_t> raw = base + 32;
-        const uint32_t n = it.n;
-        if (tid < 16) {
-          if constexpr (FT == 1 || FT == 2) {
-            if (n + tid < roundUp(n, 16)) raw[n + tid] = 0;
-          } else {
-            if (n + tid < roundUp(n, 8)) ((gp<uint16_t>)raw)[n + tid] = 0;
-            if (n + tid < roundUp(n, 16)) raw[2 * roundUp(n, 8) + n + tid] = 0;
-          }
+        gp<uint32_t> fh = (gp<uint32_t>)base;
+        fh[0] = kFloatMagicVersion;
+        fh[1] = it.n;
+        fh[2] = uint32_t(FT) | (A().useChecksum ? 0x10u : 0u);
+        fh[3] = A().useChecksum ? ckv : 0u;
+        fh[5] = 0;
+        fh[6] = 0;
+        fh[7] = 0;
+      }
+    }
+    // pdf: 4 symbols per lane, one 8 B store
+    {
+      const u32x2 pd = *(lp<const u32x2>)&pdfS[4 * lane];
+      *(gp<u32x2>)((gp<uint8_t>)(o + kANSHeaderBytes) + 8 * lane) = pd;
+    }
+    if constexpr (FT != 0) {
+      gp<uint8_t> raw = base + 32;
+      const uint32_t n = it.n;
+      if (lane < 16) {
+        if constexpr (FT == 1 || FT == 2) {
+          if (n + lane < roundUp(n, 16)) raw[n + lane] = 0;
+        } else {
+          if (n + lane < roundUp(n, 8)) ((gp<uint16_t>)raw)[n + lane] = 0;
+          if (n + lane < roundUp(n, 16)) raw[2 * roundUp(n, 8) + n + lane] = 0;
         }
       }
     }
-    __syncthreads();
-    if (tid < nk) {
-      const uint32_t k = first + tid;
+  };
+
+  // ---- placement of E by waves 1-3 (t = tid - 64 of 192), after the
+  // look-back: blockWords and the payload copy-out ----
+  auto place = [&](const PItem& it) __attribute__((always_inline)) {
+    const uint32_t tid = tidNow(), lane = laneNow();
+    (void)tid;
+    (void)lane;
+    constexpr uint32_t kPT = pc::kThreads - 64;
+    const uint32_t t = tid - 64;
+    const uint32_t first = it.x * pc::kBlocksPerItem;
+    const uint32_t nk = first < it.nBlocks ? min(pc::kBlocksPerItem, it.nBlocks - first) : 0u;
+    gp<uint8_t> o = startOf(OUT(), it.b) + (FT == 0 ? 0u : 32u + floatRawBytes(FT, it.n));  // ANS archive
+    gp<uint8_t> states = o + kANSHeaderBytes + kPdfBytes;
+    gp<uint2> bwords = (gp<uint2>)(states + uint64_t(kStateBytesPerBlock) * it.nBlocks);
+    // a poisoned element's archive is abandoned (outSize 0): its payload
+    // range is not known, so nothing more is written
+    if (nk == 0 || poisonS) return;
+    if (t < nk) {
+      const uint32_t k = first + t;
       const uint32_t uwk = min(kBlockSize, it.n - k * kBlockSize);
-      st8(bwords + k, make_uint2((uwk << 16) | cwE[tid], preE[tid]));
+      st8(bwords + k, make_uint2((uwk << 16) | cwE[t], preE[t]));
     }
-    if (nk == 0) return;
     // payload: 16 B vectors over the item's contiguous archive range; the
     // source is the block's ring, or its slot for words spilled before the end
     gp<uint4> dst = (gp<uint4>)((gp<uint8_t>)(bwords + roundUp(it.nBlocks, 2)) + 2ull * preE[0]);
     const uint32_t nv = (preE[nk - 1] + roundUp(cwE[nk - 1], 8) - preE[0]) / 8;
-    for (uint32_t v = tid; v < nv; v += pc::kThreads) {
+    for (uint32_t v = t; v < nv; v += kPT) {
       const uint32_t wd = preE[0] + 8 * v;
       uint32_t k = 0;
 #pragma unroll
@@ -564,47 +695,64 @@ __global__ __launch_bounds__(pc::kThreads) __attribute__((amdgpu_waves_per_eu(4,
     }
   };
 
-  // ---- encode E's pair (and store its states / word counts) ----
+  // ---- encode E's pair done: states to the archive, word counts to LDS ----
   auto encodeDone = [&](const PItem& it) __attribute__((always_inline)) {
-    const uint32_t uw = h ? pairSize(it, 1) : pairSize(it, 0);
+    const uint32_t hh = halfNow();
+    const uint32_t uw = laneSize(it);
     if (uw) {
       gp<uint8_t> o = startOf(OUT(), it.b) + (FT == 0 ? 0u : 32u + floatRawBytes(FT, it.n));
       gp<uint8_t> states = o + kANSHeaderBytes + kPdfBytes;
-      const uint32_t blk = it.x * pc::kBlocksPerItem + 2 * w + h;
+      const uint32_t blk = it.x * pc::kBlocksPerItem + 2 * w + hh;
       ((gp<uint32_t>)(states + uint64_t(kStateBytesPerBlock) * blk))[l] = p.x;
     }
     if (l == 0) {
-      cwE[2 * w + h] = uw ? uint32_t(h ? p.nout[1] : p.nout[0]) : 0u;
-      flE[2 * w + h] = uw ? uint32_t(h ? p.flushed[1] : p.flushed[0]) : 0u;
+      cwE[2 * w + hh] = uw ? uint32_t(hh ? p.nout[1] : p.nout[0]) : 0u;
+      flE[2 * w + hh] = uw ? uint32_t(hh ? p.flushed[1] : p.flushed[0]) : 0u;
     }
   };
+
+  // a vector with no word of the block loads from this workgroup's slot space
+  const gp<const WordT> dummy = (gp<const WordT>)slotBase;
 
   // ================= the pipeline =================
   // Only item indices live across iterations; everything else is recomputed
   // (scalar work) where it is needed.
+  // the next call on this stream (epoch + 1) counts from zero: calls on one
+  // stream run one after another, so nothing reads that counter now
+  if (blockIdx.x == 0 && tid == 0)
+    __hip_atomic_store(G(A().ctr) + ((A().epoch + 1) & 1u), 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();  // histogram zeroed
-  uint32_t iE = A().items, iL = itemAt(0), round = 0;
+  uint32_t round = 0;
+  uint32_t iE = A().items, iL = itemOfElem(elemOfRound(0));
   if (iL >= A().items) return;
-  uint32_t ckE = 0;
-  bool poisonE = false;
   while (true) {
     const bool hasE = iE < A().items, hasL = iL < A().items;
     if (!hasE && !hasL) break;
-    __builtin_amdgcn_s_setprio(0);
+    // Segment-phase wave priority rotates over the CU's dispatch slots
+    // round by round.  At equal priority the SIMD arbiter favours the older
+    // waves: the last-dispatched slot's teams ran a quarter slower and set
+    // the kernel's end (slot medians 140 / 146 / 152 / 160 us of a 169 us
+    // launch); rotating gives each slot each level in turn.  (The hand-off
+    // window runs above all of them.)
+    {
+      const uint32_t pr = (blockIdx.x / A().slotSpan + round) % 3u;
+      if (pr == 0) __builtin_amdgcn_s_setprio(0);
+      else if (pr == 1) __builtin_amdgcn_s_setprio(1);
+      else __builtin_amdgcn_s_setprio(2);
+    }
     {
       const PItem E = itemOf(iE, A(), IN()), L = itemOf(iL, A(), IN());
       const uint32_t uwE0 = pairSize(E, 0), uwE1 = pairSize(E, 1);
       const uint32_t uwL0 = pairSize(L, 0), uwL1 = pairSize(L, 1);
       // encode: the full-step variant when both blocks of the pair are whole
-      // (uwE0 >= uwE1); a poisoned item encodes nothing (uw 0: every step masked)
-      const bool encOn = hasE && uwE0 != 0 && !poisonE;
+      // (uwE0 >= uwE1)
+      const bool encOn = hasE && uwE0 != 0;
       const bool fastE = uwE1 == kBlockSize;
-      const uint32_t uwEnc = h ? uwE1 : uwE0;
+      const uint32_t uwEnc = halfNow() ? uwE1 : uwE0;
       // split: the unmasked variant when both blocks of the pair are whole
       const bool loadOn = hasL && uwL0 != 0;
       const bool fullL = uwL1 == kBlockSize;
-      const uint32_t uwL = h ? uwL1 : uwL0;
-      const gp<const WordT> elemL = (gp<const WordT>)startOf(IN(), L.b);
+      const uint32_t uwL = halfNow() ? uwL1 : uwL0;
       const gp<const WordT> srcL = srcOf(L);
       gp<uint8_t> rawL = FT == 0 ? gp<uint8_t>(nullptr) : startOf(OUT(), L.b) + 32;
       if (hasE) encInit();
@@ -619,13 +767,13 @@ __global__ __launch_bounds__(pc::kThreads) __attribute__((amdgpu_waves_per_eu(4,
         // segment of L into the symbol registers those steps freed; loads
         // run D segments ahead of the split
 #pragma unroll
-        for (uint32_t g = 0; g < uint32_t(D); ++g) load(elemL, srcL, uwL, g);
+        for (uint32_t g = 0; g < uint32_t(D); ++g) load(dummy, srcL, uwL, g);
         staticFor<pc::kSegs>([&](auto gTag) __attribute__((always_inline)) {
           constexpr uint32_t g = decltype(gTag)::value;
           encSeg(g);
           if (fullL) split(L, rawL, uwL, g, std::true_type{});
           else split(L, rawL, uwL, g, std::false_type{});
-          if (g + D < pc::kSegs) load(elemL, srcL, uwL, g + D);
+          if constexpr (g + D < pc::kSegs) load(dummy, srcL, uwL, g + D);
           __builtin_amdgcn_wave_barrier();
           transposeCount(g, uwL, (g + 1) * pc::kSegWords > uwL1);
           __builtin_amdgcn_wave_barrier();
@@ -640,20 +788,145 @@ __global__ __launch_bounds__(pc::kThreads) __attribute__((amdgpu_waves_per_eu(4,
     // The hand-offs below are on the team's critical path while the other
     // workgroups of this CU stream: they issue at raised priority (3 % of
     // the c2 launch, same-box A/B).
-    __builtin_amdgcn_s_setprio(2);
-    // E's word counts and L's histogram counts are in; E's aggregate goes out
-    // at once, so that the team's look-backs in place() rarely wait
+    __builtin_amdgcn_s_setprio(3);
+    if constexpr (kCk) {
+      if (hasL) {
+        const uint32_t c = waveXor((ck ^ (ck >> 8) ^ (ck >> 16) ^ (ck >> 24)) & 0xffu);
+        if (lane == 0) ckS[w] = c;
+      }
+      ck = 0;
+    }
+    // E's word counts and L's histogram counts are in
     __syncthreads();
-    if (hasE && w == 0) publishAgg(itemOf(iE, A(), IN()), poisonE);
-    if (hasL) publish(itemOf(iL, A(), IN()));
-    if (hasE) place(itemOf(iE, A(), IN()), poisonE, ckE);
+    if (hasL) publishHist(itemOf(iL, A(), IN()));
+    if (hasE && w == 0) publishAgg(itemOf(iE, A(), IN()));
+    // L's team: the first 16 members' partials (this thread's bin) are
+    // loaded now, in flight over E's look-back; their tags say who is in
+    constexpr uint32_t kBatch = 16;
+    uint32_t acc[kBatch], ckv = 0;
+    if (hasL) {
+      const uint32_t tid = tidNow();
+      const PItem L = itemOf(iL, A(), IN());
+      gp<const uint32_t> hp = G(A().part) + uint64_t(L.tb) * kNumSymbols + tid;
+#pragma unroll
+      for (uint32_t k = 0; k < kBatch; ++k) acc[k] = k < L.team ? ldSc1(hp + uint64_t(k) * kNumSymbols) : 0u;
+      if constexpr (kCk) ckv = tid < L.team ? ldSc1(G(A().partCk) + L.tb + tid) : 0u;
+    }
+    // (member 0, wave 0) this team's element of round + 2, taken now, if
+    // round + 1 has one
+    if (hasL && w == 0 && lane == 0) {
+      uint32_t T, X;
+      teamX(T, X);
+      if (X == 0 && elemOfRound(round + 1) < A().nb) dequeueRound(round + 2);
+    }
+    if (hasE && w == 0) lookBackE(itemOf(iE, A(), IN()));
+    // spilled words of E are read back by other waves in place(): a wave
+    // that spilled waits for its slot stores
+    if (hasE && (p.flushed[0] | p.flushed[1])) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    // L's team partials -> one count per thread (keys[tid]); then wave 0
+    // normalises L while waves 1-3 place E
+    if (hasL) {
+      const uint32_t tid = tidNow(), lane = laneNow();
+      const PItem L = itemOf(iL, A(), IN());
+      const uint32_t ep = A().epoch;
+      gp<const uint32_t> hp = G(A().part) + uint64_t(L.tb) * kNumSymbols + tid;
+      uint32_t missing = L.team >= 32 ? ~0u : (1u << L.team) - 1u;
+      bool ckMissing = kCk && tid < L.team;
+      uint32_t count = 0, ckAcc = 0;
+#pragma unroll
+      for (uint32_t k = 0; k < kBatch; ++k) {
+        if (k < L.team && (acc[k] >> 16) == ep) {
+          count += acc[k] & 0xffffu;
+          missing &= ~(1u << k);
+        }
+      }
+      if (ckMissing && (ckv >> 16) == ep) {
+        ckAcc = ckv & 0xffu;
+        ckMissing = false;
+      }
+      // the rest of the team (members >= 16; late members), polled with
+      // backoff; after the time budget (or spinCap polls) the element is
+      // counted here from its input instead
+      bool fallback = false;
+      const uint64_t t0 = realtime();
+      for (uint32_t spins = 0; __syncthreads_or(missing != 0 || ckMissing); ++spins) {
+        if (__syncthreads_or(spins >= A().spinCap || realtime() - t0 >= A().fallbackTicks)) {
+          fallback = true;
+          break;
+        }
+        if (spins) __builtin_amdgcn_s_sleep(2);
+        for (uint32_t k0 = 0; k0 < L.team; k0 += kBatch) {
+          if (((missing >> k0) & 0xffffu) == 0) continue;
+#pragma unroll
+          for (uint32_t k = 0; k < kBatch; ++k)
+            acc[k] = (missing >> (k0 + k)) & 1u ? ldSc1(hp + uint64_t(k0 + k) * kNumSymbols) : 0u;
+#pragma unroll
+          for (uint32_t k = 0; k < kBatch; ++k) {
+            if (((missing >> (k0 + k)) & 1u) && (acc[k] >> 16) == ep) {
+              count += acc[k] & 0xffffu;
+              missing &= ~(1u << (k0 + k));
+            }
+          }
+        }
+        if (ckMissing) {
+          ckv = ldSc1(G(A().partCk) + L.tb + tid);
+          if ((ckv >> 16) == ep) {
+            ckAcc = ckv & 0xffu;
+            ckMissing = false;
+          }
+        }
+      }
+      uint32_t ckL = 0;
+      if (fallback) {
+        count = countElement(L, ckL);
+      } else if (kCk && w == 0) {
+        ckL = waveXor(ckAcc);
+      }
+      keys[tid] = count;
+      // (one add per wave: the LDS counter reaches kWaves - 1)
+      if (w != 0 && lane == 0) __hip_atomic_fetch_add(&sigS, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (w == 0) {
+        while (__hip_atomic_load(&sigS, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != pc::kWaves - 1)
+          __builtin_amdgcn_s_sleep(1);
+        sigS = 0;
+        uint32_t c[4], cdf[4];
+        const u32x4 kv = *(lp<const u32x4>)&keys[4 * lane];
+        c[0] = kv.x;
+        c[1] = kv.y;
+        c[2] = kv.z;
+        c[3] = kv.w;
+        if (L.n != 0) {
+          // (scratch: the trash dwords and keys, both free in the window)
+          normalizeWave(c, cdf, L.n, A().pb, &trashS[0][0], keys);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) c[j] = cdf[j] = 0;
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint4 e = encTableEntryReg(c[j], cdf[j], A().pb);
+          *(lp<u32x4>)&tblS[4 * (4 * lane + j)] = u32x4{e.x, e.y, e.z, e.w};
+        }
+        *(lp<u32x2>)&pdfS[4 * lane] = u32x2{c[0] | (c[1] << 16), c[2] | (c[3] << 16)};
+        if (L.x == 0) {
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          writeHeadFixedL(L, ckL);
+        }
+      }
+    }
+    if (hasE && w != 0) place(itemOf(iE, A(), IN()));
+    // the next round's element (logged a round ago): lane 0 of each wave
     uint32_t iN = A().items;
     if (hasL) {
-      poisonE = barrierNormalize(itemOf(iL, A(), IN()), ckE);
-      iN = itemAt(++round);
+      uint32_t e = 0;
+      if (lane == 0) e = elemOfRound(round + 1);
+      iN = itemOfElem(readfirst(e));
     }
+    __syncthreads();
     iE = iL;
     iL = iN;
+    ++round;
   }
 }
 

@@ -16,8 +16,8 @@ namespace {
 
 struct Arena {
   std::mutex m;
-  void* ptr = nullptr;
-  size_t bytes = 0;
+  void* ptr[kSyncRegions] = {};
+  size_t bytes[kSyncRegions] = {};
   uint32_t epoch = 0;
 };
 
@@ -29,21 +29,30 @@ std::map<Key, std::unique_ptr<Arena>>& arenas() {
 }
 
 std::atomic<uint32_t> gSpinCap{1u << 24};
+std::atomic<uint32_t> gBarrierBudget{20000};
 }  // namespace
 
 void setSpinCap(uint32_t polls) { gSpinCap.store(polls); }
 uint32_t spinCap() { return gSpinCap.load(); }
+void setBarrierBudget(uint32_t ticks) { gBarrierBudget.store(ticks); }
+uint32_t barrierBudgetTicks() { return gBarrierBudget.load(); }
 
-SyncLease::SyncLease(StackDeviceMemory& res, hipStream_t stream, size_t bytes) {
+SyncLease::SyncLease(StackDeviceMemory& res, hipStream_t stream, const size_t (&bytes)[kSyncRegions]) {
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
   HIP_CHECK(hipStreamIsCapturing(stream, &cs));
   if (cs != hipStreamCaptureStatusNone) {
     // graph capture: per-call state from the caller's arena, zeroed by a
     // captured memset on every replay
     capturing = true;
-    capMem_ = res.alloc<uint8_t>(stream, bytes);
-    HIP_CHECK(hipMemsetAsync(capMem_.data(), 0, bytes, stream));
-    base = capMem_.data();
+    size_t total = 0;
+    for (int k = 0; k < kSyncRegions; ++k) total += roundUp64(std::max<size_t>(bytes[k], 8), 256);
+    capMem_ = res.alloc<uint8_t>(stream, total);
+    HIP_CHECK(hipMemsetAsync(capMem_.data(), 0, total, stream));
+    size_t off = 0;
+    for (int k = 0; k < kSyncRegions; ++k) {
+      base[k] = capMem_.data() + off;
+      off += roundUp64(std::max<size_t>(bytes[k], 8), 256);
+    }
     epoch = 1;
     return;
   }
@@ -58,25 +67,27 @@ SyncLease::SyncLease(StackDeviceMemory& res, hipStream_t stream, size_t bytes) {
     a = slot.get();
   }
   lock_ = std::unique_lock<std::mutex>(a->m);
-  bool zero = false;
-  if (a->bytes < bytes) {
-    size_t want = std::max<size_t>(64 << 10, a->bytes);
-    while (want < bytes) want *= 2;
-    if (a->ptr) {
-      HIP_CHECK(hipStreamSynchronize(stream));  // earlier calls may still read it
-      HIP_CHECK(hipFree(a->ptr));
+  bool grow = false;
+  for (int k = 0; k < kSyncRegions; ++k) grow = grow || a->bytes[k] < bytes[k];
+  if (grow) {
+    // earlier calls may still read the regions being replaced
+    HIP_CHECK(hipStreamSynchronize(stream));
+    for (int k = 0; k < kSyncRegions; ++k) {
+      if (a->bytes[k] >= bytes[k] && a->ptr[k]) continue;
+      size_t want = std::max<size_t>(64 << 10, a->bytes[k]);
+      while (want < bytes[k]) want *= 2;
+      if (a->ptr[k]) HIP_CHECK(hipFree(a->ptr[k]));
+      HIP_CHECK(hipMalloc(&a->ptr[k], want));
+      HIP_CHECK(hipMemsetAsync(a->ptr[k], 0, want, stream));
+      a->bytes[k] = want;
     }
-    HIP_CHECK(hipMalloc(&a->ptr, want));
-    a->bytes = want;
-    zero = true;
   }
   a->epoch = (a->epoch + 1) & kEpochMask;
-  if (a->epoch == 0) zero = true;  // wrapped: flags of every older epoch must go
-  if (zero) {
-    HIP_CHECK(hipMemsetAsync(a->ptr, 0, a->bytes, stream));
+  if (a->epoch == 0) {  // wrapped: words of every older epoch must go
+    for (int k = 0; k < kSyncRegions; ++k) HIP_CHECK(hipMemsetAsync(a->ptr[k], 0, a->bytes[k], stream));
     a->epoch = 1;
   }
-  base = a->ptr;
+  for (int k = 0; k < kSyncRegions; ++k) base[k] = a->ptr[k];
   epoch = a->epoch;
 }
 

@@ -1,5 +1,5 @@
 // Persistent per-(device, stream) device memory for the compressor's
-// cross-workgroup state: team-arrival flags and look-back flags of
+// cross-workgroup state: look-back flags and tagged partial histograms of
 // k_pcompress.
 //
 // Flags carry a per-call epoch instead of being zeroed before every call: a
@@ -28,17 +28,25 @@
 
 namespace dietgpu {
 
-constexpr uint32_t kEpochMask = 0x1fffffffu;  // 29-bit epochs (flag bits 60:32)
+// 16-bit epochs: look-back flags carry them in bits 47:32, tagged partial
+// histograms in bits 31:16 (the arena is re-zeroed when they wrap)
+constexpr uint32_t kEpochMask = 0xffffu;
+
+// Regions of one arena.  Each kind of epoch-tagged word lives in a region of
+// its own, so a stale word only ever overlaps a stale word of the same kind
+// (a tag collision across kinds -- say a look-back flag's value bits read as
+// a partial's epoch -- cannot happen whatever the shapes of earlier calls).
+enum SyncRegion : int { kSyncCounters = 0, kSyncFlags, kSyncPartials, kSyncLog, kSyncRegions };
 
 class SyncLease {
  public:
-  // A region of >= `bytes` zero-at-creation bytes for the current device and
-  // `stream`, and this call's epoch (1 .. kEpochMask).
-  SyncLease(StackDeviceMemory& res, hipStream_t stream, size_t bytes);
+  // Per region, >= `bytes[k]` zero-at-creation bytes for the current device
+  // and `stream`, and this call's epoch (1 .. kEpochMask).
+  SyncLease(StackDeviceMemory& res, hipStream_t stream, const size_t (&bytes)[kSyncRegions]);
   SyncLease(const SyncLease&) = delete;
   SyncLease& operator=(const SyncLease&) = delete;
 
-  void* base = nullptr;
+  void* base[kSyncRegions] = {};
   uint32_t epoch = 0;
   bool capturing = false;
 
@@ -57,5 +65,12 @@ uint32_t deviceErrorCount(bool reset);
 // every wait that has to wait fail: test hook for the error path.
 void setSpinCap(uint32_t polls);
 uint32_t spinCap();
+
+// How long (100 MHz ticks of s_memrealtime) a compressor workgroup waits for
+// its team's partial histograms before it counts the element from the input
+// itself (default 20,000 = 200 us; normal team skew is a few us).  0 makes
+// every team wait fall back at once: test hook for the slow path.
+void setBarrierBudget(uint32_t ticks);
+uint32_t barrierBudgetTicks();
 
 }  // namespace dietgpu

@@ -103,10 +103,12 @@ StackDeviceMemory makeStack(int dev, const std::optional<at::Tensor>& tempMem) {
 void checkArchiveSizes(const int32_t* sizes, int64_t n) {
   for (int64_t i = 0; i < n; ++i) {
     if (sizes[i] <= 0) {
-      const uint32_t errs = dietgpu_device_error_count(0);
+      // (read and reset, as _native.check_archive_sizes does: a later error
+      // reports only the elements abandoned since this one)
+      const uint32_t errs = dietgpu_device_error_count(1);
       TORCH_CHECK(false, "compression of batch element ", i,
                   " was abandoned (a cross-workgroup wait ran out of polls; ", errs,
-                  " element(s) counted in the device error word)");
+                  " element(s) counted in the device error word since the last report)");
     }
   }
 }

@@ -62,6 +62,18 @@ class GpuFloatCodec:
             raise RuntimeError("compressed collective: an archive failed to decode")
 
 
+def _check_sizes(sizes, what):
+    """Archive sizes seen by every rank: 0 marks an element whose compression
+    was abandoned (a bounded cross-workgroup wait ran out, see
+    dietgpu_device_error_count); no valid archive is shorter than its headers.
+    Raising here, where every rank sees the same sizes, keeps the ranks in
+    step (a zero-length slot would otherwise alias the next archive and could
+    decode into the wrong output)."""
+    bad = (torch.as_tensor(sizes) <= 0).nonzero().view(-1).tolist()
+    if bad:
+        raise RuntimeError(f"{what}: compression of element(s) {bad[:8]} was abandoned (archive size 0)")
+
+
 def _pack(comp, sizes, offs, length, dev):
     """Pack the archive rows comp[i, :sizes[i]] back to back at the 16 B
     aligned offsets `offs` (= archive_offsets(sizes)) into a buffer of
@@ -112,6 +124,7 @@ def all_gather_compressed(tensors, group=None, codec=None):
     dist.all_gather_into_tensor(allmeta, meta.view(-1), group=group)
     allmeta = allmeta.view(world, 2, k).cpu()
     asizes = allmeta[:, 1, :]
+    _check_sizes(asizes.reshape(-1), "all_gather_compressed")
     offs = archive_offsets(asizes.reshape(-1)).view(world, k)
     offs = offs - offs[:, :1]  # per-rank packing, from 0
     packed = offs[:, -1] + (asizes[:, -1] + 15) // 16 * 16
@@ -149,9 +162,13 @@ def all_to_all_compressed(tensors, group=None, codec=None):
     send = _pack(comp, sizes, torch.cumsum(lens, 0) - lens, int(lens.sum()), dev)
     meta = torch.stack([torch.tensor([t.numel() for t in flat], dtype=torch.int64), sizes],
                        dim=1).to(dev)  # row j goes to rank j
-    rmeta = torch.empty_like(meta)
-    dist.all_to_all_single(rmeta, meta, group=group)
-    rmeta = rmeta.cpu()
+    # every rank gathers the whole (source, destination) table, so a poisoned
+    # archive anywhere raises on every rank before the payload exchange
+    allmeta = torch.empty([world * world, 2], dtype=torch.int64, device=dev)
+    dist.all_gather_into_tensor(allmeta, meta, group=group)
+    allmeta = allmeta.view(world, world, 2).cpu()
+    _check_sizes(allmeta[:, :, 1].reshape(-1), "all_to_all_compressed")
+    rmeta = allmeta[:, dist.get_rank(group), :]
     rlens = (rmeta[:, 1] + 15) // 16 * 16
     recv = torch.empty(max(int(rlens.sum()), 16), dtype=torch.uint8, device=dev)
     dist.all_to_all_single(recv[: int(rlens.sum())], send[: int(lens.sum())],

@@ -185,6 +185,17 @@ uint32_t dietgpu_device_error_count(int reset);
  * forces the error path deterministically for elements of more than one
  * team member.  Passed to the kernels as an argument. */
 void dietgpu_set_spin_cap(uint32_t polls);
+/* Test hook: how long (100 MHz ticks) a single-pass compressor workgroup
+ * waits for the other members of its element's team before it counts the
+ * element's histogram from the input itself (default 20000 = 200 us).  The
+ * fallback keeps the compressor live when other kernels hold CUs; 0 forces
+ * it for every team wait (archives are unchanged). */
+void dietgpu_set_barrier_budget(uint32_t ticks);
+/* Test hook: enqueue on `stream` a kernel of `workgroups` 256-thread
+ * workgroups that each hold `lds_bytes` of LDS for `micros` microseconds
+ * (<= 1 s) and exit: compute units held by another kernel while the
+ * compressor runs. */
+int dietgpu_test_occupy(void* stream, uint32_t micros, uint32_t workgroups, uint32_t lds_bytes);
 
 #ifdef __cplusplus
 }

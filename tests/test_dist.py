@@ -147,6 +147,54 @@ def test_two_rank_gloo_compressed_collectives(tmp_path):
             assert np.array_equal(got, _a2a_input(s, rank).view(torch.int16).numpy()), (rank, s)
 
 
+class _PoisonCodec(_OracleCodec):
+    """The oracle codec with one abandoned element on rank 1 (archive size 0,
+    as a poisoned compression reports it)."""
+
+    def __init__(self, rank):
+        self.rank = rank
+
+    def compress(self, tensors):
+        comp, sizes = super().compress(tensors)
+        if self.rank == 1:
+            sizes[1] = 0
+        return comp, sizes
+
+
+def _poison_worker(rank, world, port, outdir):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from dietgpu_fork_amd import dist as D
+
+        msgs = []
+        for fn, arg in ((D.all_gather_compressed, _gather_inputs(rank)),
+                        (D.all_to_all_compressed, [_a2a_input(rank, d) for d in range(world)])):
+            try:
+                fn(arg, codec=_PoisonCodec(rank))
+                msgs.append("no error")
+            except RuntimeError as e:
+                msgs.append(str(e))
+        with open(os.path.join(outdir, f"poison{rank}.txt"), "w") as f:
+            f.write("\n".join(msgs))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_gloo_abandoned_archive_raises_everywhere(tmp_path):
+    """A size-0 (abandoned) archive on one rank makes BOTH collectives raise
+    on EVERY rank before the payload exchange (no rank left waiting, no
+    zero-length slot aliasing the next archive)."""
+    world = 2
+    mp.spawn(_poison_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    for rank in range(world):
+        msgs = (tmp_path / f"poison{rank}.txt").read_text().split("\n")
+        assert len(msgs) == 2
+        assert "all_gather_compressed" in msgs[0] and "abandoned" in msgs[0], msgs
+        assert "all_to_all_compressed" in msgs[1] and "abandoned" in msgs[1], msgs
+
+
 C5_TOTAL, C5_WORDS = 64, 257  # the c5 plan at test size (bench.py: 8192 x 524288)
 
 

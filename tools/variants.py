@@ -55,6 +55,34 @@ PRIO = [(P, "    // E's word counts and L's histogram counts are in; E's aggrega
         (P, "    if (!hasE && !hasL) break;\n", "    if (!hasE && !hasL) break;\n    __builtin_amdgcn_s_setprio(0);\n")]
 def STAG4(ticks):
     return [(P, "  if (iL >= A().items) return;\n", "  if (iL >= A().items) return;\n  {\n    const unsigned long long t0_ = __builtin_amdgcn_s_memrealtime();\n    const unsigned long long dl_ = (blockIdx.x >> 8) * %dull;\n    while (__builtin_amdgcn_s_memrealtime() - t0_ < dl_) __builtin_amdgcn_s_sleep(8);\n  }\n" % ticks)]
+# per-wave phase stamps of the three-item pipeline (round 3): stamp[(wg, iteration, wave, phase)]
+STAMP3 = [
+    (P, "namespace pc {", "__device__ unsigned long long g_stamp[4096 * 8 * 4 * 16];\n#define STAMP(ph) do { if (lane == 0 && itc < 8) { unsigned long long t_ = __builtin_amdgcn_s_memrealtime(); asm volatile(\"\" : \"+v\"(t_)); ((volatile unsigned long long*)g_stamp)[((blockIdx.x * 8 + itc) * 4 + w) * 16 + (ph)] = t_; } } while (0)\nnamespace pc {"),
+    (P, "  uint32_t round = 0;\n", "  uint32_t round = 0;\n  uint32_t itc = 0;\n"),
+    (P, "    // Segment-phase wave priority rotates", "    STAMP(0);\n    // Segment-phase wave priority rotates"),
+    (P, "    __builtin_amdgcn_s_setprio(3);\n", "    STAMP(1);\n    __builtin_amdgcn_s_setprio(3);\n"),
+    (P, "    // E's word counts and L's histogram counts are in\n    __syncthreads();\n", "    // E's word counts and L's histogram counts are in\n    __syncthreads();\n    STAMP(2);\n"),
+    (P, "    if (hasL) publishHist(itemOf(iL, A(), IN()));", "    if (hasL) publishHist(itemOf(iL, A(), IN()));\n    STAMP(8);"),
+    (P, "    if (hasE && w == 0) lookBackE(itemOf(iE, A(), IN()));", "    STAMP(3);\n    if (hasE && w == 0) lookBackE(itemOf(iE, A(), IN()));\n    STAMP(4);"),
+    (P, "      const uint32_t ep = A().epoch;", "      STAMP(5);\n      const uint32_t ep = A().epoch;"),
+    (P, "    if (hasE && w != 0) place(itemOf(iE, A(), IN()));", "    if (hasE && w != 0) place(itemOf(iE, A(), IN()));\n    STAMP(6);"),
+    (P, "        if (L.x == 0) {\n          asm volatile", "        STAMP(7);\n        if (L.x == 0) {\n          asm volatile"),
+    (P, "      keys[tid] = count;\n", "      keys[tid] = count;\n      STAMP(10);\n"),
+    (P, "    iE = iL;\n", "    STAMP(9);\n    ++itc;\n    iE = iL;\n"),
+    ("codec.hip", "uint32_t deviceErrorCount(bool reset) {", "extern \"C\" void* dietgpu_debug_stamps() { void* p = nullptr; (void)hipGetSymbolAddress(&p, HIP_SYMBOL(g_stamp)); return p; }\n\nuint32_t deviceErrorCount(bool reset) {"),
+]
+# round-3 attribution variants of the three-item pipeline (outputs invalid)
+V3NOENC = [(P, "const bool encOn = hasE && uwE0 != 0;", "const bool encOn = false;")]
+V3NOHIST = [(P, "__hip_atomic_fetch_add(hcol + __umul24(sym, pc::kHistStride), 1u, __ATOMIC_RELAXED,\n                               __HIP_MEMORY_SCOPE_WORKGROUP);",
+             "if (sym == 0x1234u) __hip_atomic_fetch_add(hcol + __umul24(sym, pc::kHistStride), 1u, __ATOMIC_RELAXED,\n                               __HIP_MEMORY_SCOPE_WORKGROUP);"),
+            (P, "__hip_atomic_fetch_add(hcol + __umul24(sym, pc::kHistStride), add, __ATOMIC_RELAXED,",
+             "if (sym == 0x1234u) __hip_atomic_fetch_add(hcol + __umul24(sym, pc::kHistStride), add, __ATOMIC_RELAXED,")]
+V3NOSPLITST = [(P, "splitVec<FT>(v, i0, it.n, raw, myT + off, myT + off, store);", "splitVec<FT>(v, i0, it.n, raw, myT + off, myT + off, false);")]
+# segment-phase priority schedules (round 3)
+PRLINE = "      const uint32_t pr = (blockIdx.x / A().slotSpan + round) % 3u;"
+def PRIO3(expr):
+    return [(P, PRLINE, "      const uint32_t pr = " + expr + ";"),
+            (P, "      else __builtin_amdgcn_s_setprio(2);\n    }", "      else if (pr == 2) __builtin_amdgcn_s_setprio(2);\n      else __builtin_amdgcn_s_setprio(3);\n    }")]
 SP = "sparse.hip"
 VARS = {
     "encprio": [("encode.h", "    // every wave's slot stores are complete before other waves copy them\n    asm volatile(\"s_waitcnt vmcnt(0)\" ::: \"memory\");", "    __builtin_amdgcn_s_setprio(2);\n    // every wave's slot stores are complete before other waves copy them\n    asm volatile(\"s_waitcnt vmcnt(0)\" ::: \"memory\");")],
@@ -74,6 +102,16 @@ VARS = {
     "stag10": STAG(1000),
     "stag16": STAG(1600),
     "stamp2": STAMP2,
+    "stamp3": STAMP3,
+    "v3noenc": V3NOENC,
+    "v3nohist": V3NOHIST,
+    "v3nosplitst": V3NOSPLITST,
+    "v3noencnohist": V3NOENC + V3NOHIST,
+    "pr4rot": PRIO3("(blockIdx.x / A().slotSpan + round) & 3u"),
+    "prslot": PRIO3("(blockIdx.x / A().slotSpan) & 3u"),
+    "prhalf": PRIO3("(blockIdx.x / A().slotSpan) >> 1"),
+    "prhalfalt": PRIO3("((blockIdx.x / A().slotSpan) >> 1) ^ (round & 1u)"),
+    "pr3rotrev": PRIO3("(3u - (blockIdx.x / A().slotSpan) + round) % 3u"),
     "stamp": STAMP,
     "noenc_nohist": [NOENC] + NOHIST,
     "noenc_nohist_nosplitst": [NOENC, NOSPLITST] + NOHIST,
