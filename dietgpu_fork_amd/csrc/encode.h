@@ -246,12 +246,19 @@ __device__ __forceinline__ uint32_t normalizeCount(uint32_t count, uint32_t tota
 }
 
 // The same normalisation by ONE wave, lane l holding symbols 4l + j
-// (j < 4): no workgroup barrier, so the other waves of a workgroup can work
-// meanwhile.  c[j]: the counts in, the pdfs out; cdf[j]: the exclusive
-// cumulative pdfs (symbol order).  total > 0.  keysL, byRank: 256 words of
-// LDS each, private to this wave during the call.
-__device__ __forceinline__ void normalizeWave(uint32_t (&c)[4], uint32_t (&cdf)[4], uint32_t total, int pb,
-                                              uint32_t* keysL, uint32_t* byRank) {
+// (j < 4), in registers only: no workgroup barrier (the other waves of a
+// workgroup work meanwhile) and no LDS round trip (queued behind the other
+// workgroups' traffic, a dozen of them took microseconds).  c[j]: the
+// counts in, the pdfs out; cdf[j]: the exclusive cumulative pdfs (symbol
+// order).  total > 0.
+//   Ranks: the keys (q << 16) | s of the g0 entries with q > 1 (the only ones
+// ever decremented) are broadcast one at a time with v_readlane (g0 is a few
+// dozen); rank = number of larger keys, i.e. the position in the
+// reference's descending sort.  Rounds: the reference decrements ranks
+// [g - k, g) of the g entries still > 1; those always form a prefix of the
+// ranks (values stay in descending rank order: only the lowest-ranked are
+// ever lowered), so an entry tests its own rank against g in place.
+__device__ __forceinline__ void normalizeWave(uint32_t (&c)[4], uint32_t (&cdf)[4], uint32_t total, int pb) {
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t W = 1u << pb;
   uint32_t q[4];
@@ -267,57 +274,34 @@ __device__ __forceinline__ void normalizeWave(uint32_t (&c)[4], uint32_t (&cdf)[
     for (int j = 0; j < 4; ++j)
       q[j] += uint32_t(diff) / kNumSymbols + (4 * lane + j < uint32_t(diff) % kNumSymbols ? 1u : 0u);
   } else if (diff < 0) {
-    // keys (q << 16) | s of the entries with q > 1 (the only ones ever
-    // decremented: a prefix [0, g) of the descending order), compacted into
-    // keysL; each one's rank = number of larger keys
-    uint32_t g0 = 0, key[4];
+    uint32_t key[4], rank[4] = {0, 0, 0, 0};
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      key[j] = (q[j] << 16) | (4 * lane + j);
-      const uint64_t m = ballot(q[j] > 1);
-      if (q[j] > 1) keysL[g0 + mbcnt(m)] = key[j];
-      g0 += uint32_t(__popcll(m));
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_wave_barrier();
-    uint32_t rank[4] = {0, 0, 0, 0};
-    for (uint32_t t = 0; t < g0; ++t) {
-      const uint32_t k = keysL[t];
+    for (int j = 0; j < 4; ++j) key[j] = (q[j] << 16) | (4 * lane + j);
+    auto countAbove = [&](uint32_t kj, uint64_t m) __attribute__((always_inline)) {
+      while (m) {
+        const uint32_t src = uint32_t(__builtin_ctzll(m));
+        m &= m - 1;
+        const uint32_t kb = uint32_t(__builtin_amdgcn_readlane(int(kj), int(src)));
 #pragma unroll
-      for (int j = 0; j < 4; ++j) rank[j] += k > key[j] ? 1u : 0u;
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-      if (q[j] > 1) byRank[rank[j]] = q[j];
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_wave_barrier();
-    // the reference's rounds: each takes 1 from the k = min(d, g) lowest-
-    // ranked of the g entries still > 1 (entry r = lane + 64 i)
-    uint32_t Q[kNumSymbols / 64];
-#pragma unroll
-    for (uint32_t i = 0; i < kNumSymbols / 64; ++i) Q[i] = lane + 64 * i < g0 ? byRank[lane + 64 * i] : 1u;
+        for (int j = 0; j < 4; ++j) rank[j] += kb > key[j] ? 1u : 0u;
+      }
+    };
+    countAbove(key[0], ballot(q[0] > 1));
+    countAbove(key[1], ballot(q[1] > 1));
+    countAbove(key[2], ballot(q[2] > 1));
+    countAbove(key[3], ballot(q[3] > 1));
     int d = -diff;
     while (d > 0) {
       int g = 0;
 #pragma unroll
-      for (uint32_t i = 0; i < kNumSymbols / 64; ++i) g += __popcll(ballot(Q[i] > 1));
+      for (int j = 0; j < 4; ++j) g += __popcll(ballot(q[j] > 1));
       if (g == 0) break;  // reference asserts; unreachable for real tables
       const int k = d < g ? d : g;
 #pragma unroll
-      for (uint32_t i = 0; i < kNumSymbols / 64; ++i) {
-        const int r = int(lane + 64 * i);
-        if (r >= g - k && r < g) Q[i] -= 1;
-      }
+      for (int j = 0; j < 4; ++j)
+        if (q[j] > 1 && int(rank[j]) >= g - k) q[j] -= 1;
       d -= k;
     }
-#pragma unroll
-    for (uint32_t i = 0; i < kNumSymbols / 64; ++i)
-      if (lane + 64 * i < g0) byRank[lane + 64 * i] = Q[i];
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_wave_barrier();
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-      if (q[j] > 1) q[j] = byRank[rank[j]];
   }
   const uint32_t lsum = q[0] + q[1] + q[2] + q[3];
   const uint32_t base = waveInclusiveScan(lsum) - lsum;

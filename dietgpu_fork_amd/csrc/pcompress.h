@@ -208,13 +208,13 @@ __global__ __launch_bounds__(pc::kThreads) __attribute__((amdgpu_waves_per_eu(4,
   __shared__ __attribute__((aligned(16))) uint16_t rings[pc::kBlocksPerItem * pc::kRing];
   __shared__ __attribute__((aligned(16))) uint32_t tblS[kNumSymbols * 4];
   __shared__ __attribute__((aligned(16))) uint8_t symT[pc::kBlocksPerItem][pc::kSegWords];
-  __shared__ uint32_t trashS[pc::kWaves][64];
-  __shared__ __attribute__((aligned(16))) uint32_t keys[kNumSymbols];
+  __shared__ __attribute__((aligned(16))) uint32_t trashS[pc::kWaves][64];
   __shared__ __attribute__((aligned(16))) uint16_t pdfS[kNumSymbols];
-  __shared__ uint32_t red[pc::kWaves];
   __shared__ uint32_t ckS[pc::kWaves];
-  __shared__ uint32_t cwE[pc::kBlocksPerItem], flE[pc::kBlocksPerItem], preE[pc::kBlocksPerItem];
-  __shared__ uint32_t poisonS, sigS;
+  __shared__ __attribute__((aligned(16))) uint32_t cwE[pc::kBlocksPerItem];
+  __shared__ __attribute__((aligned(16))) uint32_t flE[pc::kBlocksPerItem];
+  __shared__ __attribute__((aligned(16))) uint32_t preE[pc::kBlocksPerItem];
+  __shared__ uint32_t poisonS, sigS, fbS;
 
   const uint32_t tid = threadIdx.x;
   // the lane's half (0: lanes 0-31, 1: lanes 32-63), recomputed at each use
@@ -250,7 +250,7 @@ __global__ __launch_bounds__(pc::kThreads) __attribute__((amdgpu_waves_per_eu(4,
 
   for (uint32_t i = tid; i < pc::kHistWords / 4; i += pc::kThreads)
     *(lp<u32x4>)&hist[4 * i] = u32x4{0, 0, 0, 0};
-  if (tid == 0) sigS = 0;
+  if (tid == 0) sigS = fbS = 0;
   static_assert(pc::kHistWords % 4 == 0, "16 B zeroing");
   static_assert(pc::kSpill + 32 * enc::kUnroll <= pc::kRing, "ring overflow between spill checks");
 
@@ -511,43 +511,41 @@ __global__ __launch_bounds__(pc::kThreads) __attribute__((amdgpu_waves_per_eu(4,
     }
   };
 
-  // ---- slow path: L's element counted by this workgroup from its input ----
-  // (the team did not complete within the budget).  Returns this thread's
-  // bin count; ckOut: the element's byte checksum (kCk).  hist is zero on
-  // entry and on exit.
-  auto countElement = [&](const PItem& it, uint32_t& ckOut) __attribute__((always_inline)) -> uint32_t {
-    const uint32_t tid = tidNow(), lane = laneNow();
-    (void)tid;
-    (void)lane;
+  // ---- slow path (wave 0 alone): L's element counted from its input, the
+  // team having not completed within the budget.  c[j]: the count of symbol
+  // 4 lane + j; ckOut: the element's byte checksum (kCk).  The histogram's
+  // LDS is zero on entry and on exit (no other wave touches it meanwhile).
+  auto countElementWave = [&](const PItem& it, uint32_t (&c)[4], uint32_t& ckOut) __attribute__((always_inline)) {
+    const uint32_t lane = laneNow();
     const gp<const WordT> src = (gp<const WordT>)startOf(IN(), it.b);
     const uint32_t nv = divUp(it.n, kWPV);
-    uint32_t c = 0;
-    for (uint32_t v = tid; v < nv; v += pc::kThreads) {
-      const uint4 x = ld16(src + uint64_t(v) * kWPV);
-      const WordT* ws = reinterpret_cast<const WordT*>(&x);
+    lp<uint32_t> col = (lp<uint32_t>)&hist[lane & (pc::kHistCols - 1)];
+    uint32_t x = 0;
+    for (uint32_t v = lane; v < nv; v += 64) {
+      const uint4 q = ld16(src + uint64_t(v) * kWPV);
+      const WordT* ws = reinterpret_cast<const WordT*>(&q);
 #pragma unroll
       for (uint32_t k = 0; k < kWPV; ++k) {
         if (v * kWPV + k < it.n) {
-          __hip_atomic_fetch_add(hcol + __umul24(compOf<FT>(ws[k], 0), pc::kHistStride), 1u, __ATOMIC_RELAXED,
+          __hip_atomic_fetch_add(col + __umul24(compOf<FT>(ws[k], 0), pc::kHistStride), 1u, __ATOMIC_RELAXED,
                                  __HIP_MEMORY_SCOPE_WORKGROUP);
-          if constexpr (kCk) c ^= uint32_t(ws[k]);
+          if constexpr (kCk) x ^= uint32_t(ws[k]);
         }
       }
     }
-    if constexpr (kCk) {
-      c = waveXor(c);
-      if (lane == 0) red[w] = c;
-    }
-    __syncthreads();
-    uint32_t cnt = 0;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
 #pragma unroll
-    for (uint32_t k = 0; k < pc::kHistCols; ++k) {
-      cnt += hist[tid * pc::kHistStride + k];
-      hist[tid * pc::kHistStride + k] = 0;
+    for (uint32_t j = 0; j < 4; ++j) {
+      const uint32_t bin = 4 * lane + j;
+      c[j] = 0;
+#pragma unroll
+      for (uint32_t k = 0; k < pc::kHistCols; ++k) {
+        c[j] += hist[bin * pc::kHistStride + k];
+        hist[bin * pc::kHistStride + k] = 0;
+      }
     }
-    if constexpr (kCk) ckOut = red[0] ^ red[1] ^ red[2] ^ red[3];
-    __syncthreads();
-    return cnt;
+    if constexpr (kCk) ckOut = waveXor(x);
   };
 
   // ---- E's aggregate (its words, rounded to 8 per block) -> its look-back flag ----
@@ -800,17 +798,26 @@ __global__ __launch_bounds__(pc::kThreads) __attribute__((amdgpu_waves_per_eu(4,
     __syncthreads();
     if (hasL) publishHist(itemOf(iL, A(), IN()));
     if (hasE && w == 0) publishAgg(itemOf(iE, A(), IN()));
-    // L's team: the first 16 members' partials (this thread's bin) are
-    // loaded now, in flight over E's look-back; their tags say who is in
-    constexpr uint32_t kBatch = 16;
-    uint32_t acc[kBatch], ckv = 0;
+    // L's team partials: wave w gathers members w, w + 4, ... (16 B = four
+    // bins per lane: a lane holds bins 4l .. 4l + 3, the layout the one-wave
+    // normalisation takes); the first four of each wave's members are loaded
+    // now, in flight over E's look-back; their tags say who is in
+    constexpr uint32_t kPer = pc::kMaxTeam / pc::kWaves;  // members per wave
+    constexpr uint32_t kFirst = 4;                         // loaded before the barrier
+    u32x4 pa[kFirst];
+    uint32_t ckv = 0;
     if (hasL) {
-      const uint32_t tid = tidNow();
+      const uint32_t lane = laneNow();
       const PItem L = itemOf(iL, A(), IN());
-      gp<const uint32_t> hp = G(A().part) + uint64_t(L.tb) * kNumSymbols + tid;
+      gp<const u32x4> hp = (gp<const u32x4>)(G(A().part) + uint64_t(L.tb) * kNumSymbols) + lane;
 #pragma unroll
-      for (uint32_t k = 0; k < kBatch; ++k) acc[k] = k < L.team ? ldSc1(hp + uint64_t(k) * kNumSymbols) : 0u;
-      if constexpr (kCk) ckv = tid < L.team ? ldSc1(G(A().partCk) + L.tb + tid) : 0u;
+      for (uint32_t m = 0; m < kFirst; ++m) {
+        const uint32_t k = w + pc::kWaves * m;
+        pa[m] = k < L.team ? ldSc1x4(hp + uint64_t(k) * (kNumSymbols / 4)) : u32x4{0, 0, 0, 0};
+      }
+      if constexpr (kCk) {
+        if (w == 0) ckv = lane < L.team ? ldSc1(G(A().partCk) + L.tb + lane) : 0u;
+      }
     }
     // (member 0, wave 0) this team's element of round + 2, taken now, if
     // round + 1 has one
@@ -819,86 +826,108 @@ __global__ __launch_bounds__(pc::kThreads) __attribute__((amdgpu_waves_per_eu(4,
       teamX(T, X);
       if (X == 0 && elemOfRound(round + 1) < A().nb) dequeueRound(round + 2);
     }
+    // the next round's element: its log entry (written a round ago) read
+    // now, by lane 0 of each wave, in flight over the rest of the window
+    uint64_t nextRaw = 0;
+    if (hasL && lane == 0 && round + 1 >= 2 && round + 1 < A().maxR) {
+      uint32_t T, X;
+      teamX(T, X);
+      nextRaw = __hip_atomic_load(G(A().elog) + uint64_t(T) * A().maxR + round + 1, __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_AGENT);
+    }
     if (hasE && w == 0) lookBackE(itemOf(iE, A(), IN()));
     // spilled words of E are read back by other waves in place(): a wave
     // that spilled waits for its slot stores
     if (hasE && (p.flushed[0] | p.flushed[1])) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    // L's team partials -> one count per thread (keys[tid]); then wave 0
-    // normalises L while waves 1-3 place E
+    // L's team partials -> per-wave sums (LDS, the zeroed histogram's first
+    // 4 KB); wave 0 adds them and normalises L while waves 1-3 place E
     if (hasL) {
-      const uint32_t tid = tidNow(), lane = laneNow();
+      const uint32_t lane = laneNow();
       const PItem L = itemOf(iL, A(), IN());
       const uint32_t ep = A().epoch;
-      gp<const uint32_t> hp = G(A().part) + uint64_t(L.tb) * kNumSymbols + tid;
-      uint32_t missing = L.team >= 32 ? ~0u : (1u << L.team) - 1u;
-      bool ckMissing = kCk && tid < L.team;
-      uint32_t count = 0, ckAcc = 0;
+      gp<const u32x4> hp = (gp<const u32x4>)(G(A().part) + uint64_t(L.tb) * kNumSymbols) + lane;
+      auto tagged = [&](const u32x4& v) __attribute__((always_inline)) -> bool {
+        return (v.x >> 16) == ep && (v.y >> 16) == ep && (v.z >> 16) == ep && (v.w >> 16) == ep;
+      };
+      uint32_t c[4] = {0, 0, 0, 0};
+      uint32_t miss = 0;  // bit m: member w + 4 m not yet summed (this lane)
+      auto take = [&](const u32x4& v) __attribute__((always_inline)) {
+        c[0] += v.x & 0xffffu;
+        c[1] += v.y & 0xffffu;
+        c[2] += v.z & 0xffffu;
+        c[3] += v.w & 0xffffu;
+      };
 #pragma unroll
-      for (uint32_t k = 0; k < kBatch; ++k) {
-        if (k < L.team && (acc[k] >> 16) == ep) {
-          count += acc[k] & 0xffffu;
-          missing &= ~(1u << k);
-        }
+      for (uint32_t m = 0; m < kPer; ++m) {
+        const uint32_t k = w + pc::kWaves * m;
+        if (k >= L.team) continue;
+        if (m < kFirst && tagged(pa[m])) take(pa[m]);
+        else miss |= 1u << m;
       }
+      bool ckMissing = kCk && w == 0 && lane < L.team;
+      uint32_t ckAcc = 0;
       if (ckMissing && (ckv >> 16) == ep) {
         ckAcc = ckv & 0xffu;
         ckMissing = false;
       }
-      // the rest of the team (members >= 16; late members), polled with
-      // backoff; after the time budget (or spinCap polls) the element is
-      // counted here from its input instead
-      bool fallback = false;
+      // the rest (members >= 16, late members), polled with backoff; after
+      // the time budget (or spinCap polls) this wave gives up and the element
+      // is counted from its input instead
+      bool giveUp = false;
       const uint64_t t0 = realtime();
-      for (uint32_t spins = 0; __syncthreads_or(missing != 0 || ckMissing); ++spins) {
-        if (__syncthreads_or(spins >= A().spinCap || realtime() - t0 >= A().fallbackTicks)) {
-          fallback = true;
+      for (uint32_t spins = 0; ballot(miss != 0 || ckMissing) != 0; ++spins) {
+        if (spins >= A().spinCap || realtime() - t0 >= A().fallbackTicks) {
+          giveUp = true;
           break;
         }
         if (spins) __builtin_amdgcn_s_sleep(2);
-        for (uint32_t k0 = 0; k0 < L.team; k0 += kBatch) {
-          if (((missing >> k0) & 0xffffu) == 0) continue;
 #pragma unroll
-          for (uint32_t k = 0; k < kBatch; ++k)
-            acc[k] = (missing >> (k0 + k)) & 1u ? ldSc1(hp + uint64_t(k0 + k) * kNumSymbols) : 0u;
-#pragma unroll
-          for (uint32_t k = 0; k < kBatch; ++k) {
-            if (((missing >> (k0 + k)) & 1u) && (acc[k] >> 16) == ep) {
-              count += acc[k] & 0xffffu;
-              missing &= ~(1u << (k0 + k));
+        for (uint32_t m = 0; m < kPer; ++m) {
+          if ((miss >> m) & 1u) {
+            const u32x4 v = ldSc1x4(hp + uint64_t(w + pc::kWaves * m) * (kNumSymbols / 4));
+            if (tagged(v)) {
+              take(v);
+              miss &= ~(1u << m);
             }
           }
         }
         if (ckMissing) {
-          ckv = ldSc1(G(A().partCk) + L.tb + tid);
+          ckv = ldSc1(G(A().partCk) + L.tb + lane);
           if ((ckv >> 16) == ep) {
             ckAcc = ckv & 0xffu;
             ckMissing = false;
           }
         }
       }
-      uint32_t ckL = 0;
-      if (fallback) {
-        count = countElement(L, ckL);
-      } else if (kCk && w == 0) {
-        ckL = waveXor(ckAcc);
-      }
-      keys[tid] = count;
-      // (one add per wave: the LDS counter reaches kWaves - 1)
-      if (w != 0 && lane == 0) __hip_atomic_fetch_add(&sigS, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-      if (w == 0) {
+      lp<u32x4> red4 = (lp<u32x4>)&hist[0];  // [wave][64 lanes] (the histogram is zero here)
+      if (w != 0) {
+        red4[w * 64 + lane] = u32x4{c[0], c[1], c[2], c[3]};
+        if (giveUp && lane == 0) __hip_atomic_store(&fbS, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        // (one add per wave: the LDS counter reaches kWaves - 1)
+        if (lane == 0) __hip_atomic_fetch_add(&sigS, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      } else {
         while (__hip_atomic_load(&sigS, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != pc::kWaves - 1)
           __builtin_amdgcn_s_sleep(1);
         sigS = 0;
-        uint32_t c[4], cdf[4];
-        const u32x4 kv = *(lp<const u32x4>)&keys[4 * lane];
-        c[0] = kv.x;
-        c[1] = kv.y;
-        c[2] = kv.z;
-        c[3] = kv.w;
+        uint32_t ckL = kCk ? waveXor(ckAcc) : 0u;
+        const bool fb = giveUp || __hip_atomic_load(&fbS, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 0;
+#pragma unroll
+        for (uint32_t v = 1; v < pc::kWaves; ++v) {
+          const u32x4 o = red4[v * 64 + lane];
+          c[0] += o.x;
+          c[1] += o.y;
+          c[2] += o.z;
+          c[3] += o.w;
+          red4[v * 64 + lane] = u32x4{0, 0, 0, 0};
+        }
+        if (fb) {
+          fbS = 0;
+          countElementWave(L, c, ckL);
+        }
+        uint32_t cdf[4];
         if (L.n != 0) {
-          // (scratch: the trash dwords and keys, both free in the window)
-          normalizeWave(c, cdf, L.n, A().pb, &trashS[0][0], keys);
+          normalizeWave(c, cdf, L.n, A().pb);
         } else {
 #pragma unroll
           for (int j = 0; j < 4; ++j) c[j] = cdf[j] = 0;
@@ -920,7 +949,9 @@ __global__ __launch_bounds__(pc::kThreads) __attribute__((amdgpu_waves_per_eu(4,
     uint32_t iN = A().items;
     if (hasL) {
       uint32_t e = 0;
-      if (lane == 0) e = elemOfRound(round + 1);
+      if (lane == 0) {
+        e = uint32_t(nextRaw >> 32) == A().epoch ? min(uint32_t(nextRaw), A().nb) : elemOfRound(round + 1);
+      }
       iN = itemOfElem(readfirst(e));
     }
     __syncthreads();

@@ -67,7 +67,7 @@ STAMP3 = [
     (P, "      const uint32_t ep = A().epoch;", "      STAMP(5);\n      const uint32_t ep = A().epoch;"),
     (P, "    if (hasE && w != 0) place(itemOf(iE, A(), IN()));", "    if (hasE && w != 0) place(itemOf(iE, A(), IN()));\n    STAMP(6);"),
     (P, "        if (L.x == 0) {\n          asm volatile", "        STAMP(7);\n        if (L.x == 0) {\n          asm volatile"),
-    (P, "      keys[tid] = count;\n", "      keys[tid] = count;\n      STAMP(10);\n"),
+    (P, "      lp<u32x4> red4 = (lp<u32x4>)&hist[0];", "      STAMP(10);\n      lp<u32x4> red4 = (lp<u32x4>)&hist[0];"),
     (P, "    iE = iL;\n", "    STAMP(9);\n    ++itc;\n    iE = iL;\n"),
     ("codec.hip", "uint32_t deviceErrorCount(bool reset) {", "extern \"C\" void* dietgpu_debug_stamps() { void* p = nullptr; (void)hipGetSymbolAddress(&p, HIP_SYMBOL(g_stamp)); return p; }\n\nuint32_t deviceErrorCount(bool reset) {"),
 ]
