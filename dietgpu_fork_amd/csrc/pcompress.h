@@ -11,14 +11,19 @@
 //
 // Work items.  An item is 8 consecutive 4 KiB blocks of one element (one
 // block pair per wave); the items of an element form its team.  The grid is
-// at most one generation of resident workgroups, a whole number of teams, and
-// the items are dealt out in rounds of one grid: workgroup w takes item
-// r * grid + j(w) in round r.  j(w) keeps each team on one XCD (workgroups
-// w, w + 8, ... share one under the observed round-robin placement), so the
-// team's hand-offs stay in one L2 (speed only, never correctness), and gives
-// the members of a team increasing workgroup indices.  No atomics hand out
-// work: a shared work-queue counter serialises at ~90 dequeues per
-// microsecond, 11 us per round of 1024 workgroups.
+// at most one generation of resident workgroups, a whole number of teams of
+// workgroups, and a workgroup team takes one element per round: member x of
+// team T works item x of the team's element.  Team membership keeps each
+// team on one XCD (workgroups w, w + 8, ... share one under the observed
+// round-robin placement), so the team's hand-offs stay in one L2 (speed
+// only, never correctness), and gives the members increasing workgroup
+// indices.  Elements of rounds 0 and 1 are static (r * teams + T); from
+// round 2 on, member 0 takes the team's element two rounds ahead with one
+// returning add on a per-call counter and logs it (epoch-tagged) for the
+// other members, so teams that ran fast take more elements.  One add per
+// team and round (not per workgroup: a shared counter serialises at ~90
+// dequeues per microsecond), issued in one round's hand-off window and read
+// a round later, off every critical path.
 //
 // Pipeline.  A workgroup holds two items: E, whose table is known and which it
 // encodes, and L (its next round's item), which it loads.  Per iteration,

@@ -83,6 +83,30 @@ PRLINE = "      const uint32_t pr = (blockIdx.x / A().slotSpan + round) % 3u;"
 def PRIO3(expr):
     return [(P, PRLINE, "      const uint32_t pr = " + expr + ";"),
             (P, "      else __builtin_amdgcn_s_setprio(2);\n    }", "      else if (pr == 2) __builtin_amdgcn_s_setprio(2);\n      else __builtin_amdgcn_s_setprio(3);\n    }")]
+# round-3 window ablations (relative to the deferred-dequeue source)
+POLL_PAR = """        // the first four members' missing rows in flight at once, into
+        // their (now free) first-load registers; later members one by one
+#pragma unroll
+        for (uint32_t m = 0; m < kFirst; ++m)
+          if (ballot((miss >> m) & 1u) != 0) pa[m] = ldSc1x4(hp + uint64_t(w + pc::kWaves * m) * (kNumSymbols / 4));
+#pragma unroll
+        for (uint32_t m = 0; m < kPer; ++m) {
+          if ((miss >> m) & 1u) {
+            const u32x4 v = m < kFirst ? pa[m] : ldSc1x4(hp + uint64_t(w + pc::kWaves * m) * (kNumSymbols / 4));"""
+POLL_SER = """#pragma unroll
+        for (uint32_t m = 0; m < kPer; ++m) {
+          if ((miss >> m) & 1u) {
+            const u32x4 v = ldSc1x4(hp + uint64_t(w + pc::kWaves * m) * (kNumSymbols / 4));"""
+DEQ_A = """        deq = uint32_t(__hip_atomic_fetch_add(G(A().ctr) + (A().epoch & 1u) + z, 1ull, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT));"""
+DEQ_EARLY = DEQ_A + """
+      if (deq != ~0u)
+        __hip_atomic_store(G(A().elog) + uint64_t(T) * A().maxR + round + 2,
+                           (uint64_t(A().epoch) << 32) | min(2 * (A().grid / A().team) + deq, A().nb),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);"""
+R_POLL = [(P, POLL_PAR, POLL_SER)]
+R_DEQ = [(P, DEQ_A, DEQ_EARLY), (P, "      if (d != ~0u && lane == 0) {", "      if (d != ~0u && lane == 0 && d == 0x7fffffffu) {")]
+R_Z = [(P, "(A().epoch & 1u) + z, 1ull", "(A().epoch & 1u), 1ull")]
 SP = "sparse.hip"
 VARS = {
     "encprio": [("encode.h", "    // every wave's slot stores are complete before other waves copy them\n    asm volatile(\"s_waitcnt vmcnt(0)\" ::: \"memory\");", "    __builtin_amdgcn_s_setprio(2);\n    // every wave's slot stores are complete before other waves copy them\n    asm volatile(\"s_waitcnt vmcnt(0)\" ::: \"memory\");")],
@@ -113,6 +137,10 @@ VARS = {
     "prhalfalt": PRIO3("((blockIdx.x / A().slotSpan) >> 1) ^ (round & 1u)"),
     "pr3rotrev": PRIO3("(3u - (blockIdx.x / A().slotSpan) + round) % 3u"),
     "stamp": STAMP,
+    "r_poll": R_POLL,
+    "r_deq": R_DEQ,
+    "r_z": R_Z,
+    "r_all3": R_POLL + R_DEQ + R_Z,
     "noenc_nohist": [NOENC] + NOHIST,
     "noenc_nohist_nosplitst": [NOENC, NOSPLITST] + NOHIST,
     "noenc_nonorm": [NOENC] + NONORM,
