@@ -431,20 +431,28 @@ def _extras(dev, pb, reps=3):
                      lambda: C.float_decompress_pointer(row, [y], prob_bits=pb, ws=ws))
     record("c4: 1 x 128 MiB fp64 N(0,1), two ANS passes", x.numel() * 8, int(sizes[0]), tc, td, exact,
            kernels_ms=kern)
-    g = torch.Generator(device=dev).manual_seed(5)
-    f = torch.randn(15000000, generator=g, device=dev)
-    f[torch.rand(f.numel(), generator=g, device=dev) < 0.9] = 0.0
-    arch, sizes = C.sparse_compress([f], prob_bits=pb, ws=ws)
-    y = torch.empty_like(f)
-    row = [arch[0]]
-    ok, _ = C.sparse_decompress(row, [y], prob_bits=pb, ws=ws)
-    tc = _timed(lambda: C.sparse_compress([f], prob_bits=pb, ws=ws), reps)
-    td = _timed(lambda: C.sparse_decompress(row, [y], prob_bits=pb, ws=ws), reps)
-    exact = int(ok[0]) == 1 and torch.equal(f.view(torch.int32), y.view(torch.int32))
-    kern = breakdown(lambda: C.sparse_compress([f], prob_bits=pb, ws=ws),
-                     lambda: C.sparse_decompress(row, [y], prob_bits=pb, ws=ws))
-    record("c4: 1 x 15M fp32, 90 % zeros (sparse bitmap + dense codec)", f.numel() * 4, int(sizes[0]),
-           tc, td, exact, kernels_ms=kern)
+    # sparse: the reference's SparseFloatBenchmark shape (15M words, 90 %
+    # zeros) at batch 1 and 5
+    for nbs in (1, 5):
+        g = torch.Generator(device=dev).manual_seed(5)
+        fs = []
+        for _ in range(nbs):
+            f = torch.randn(15000000, generator=g, device=dev)
+            f[torch.rand(f.numel(), generator=g, device=dev) < 0.9] = 0.0
+            fs.append(f)
+        arch, sizes = C.sparse_compress(fs, prob_bits=pb, ws=ws)
+        ys = [torch.empty_like(f) for f in fs]
+        rows = [arch[i, : int(sizes[i])] for i in range(nbs)]
+        ok, _ = C.sparse_decompress(rows, ys, prob_bits=pb, ws=ws)
+        tc = _timed(lambda: C.sparse_compress(fs, prob_bits=pb, ws=ws), reps)
+        td = _timed(lambda: C.sparse_decompress(rows, ys, prob_bits=pb, ws=ws), reps)
+        exact = bool((ok == 1).all()) and all(torch.equal(a.view(torch.int32), b.view(torch.int32))
+                                              for a, b in zip(fs, ys))
+        kern = breakdown(lambda: C.sparse_compress(fs, prob_bits=pb, ws=ws),
+                         lambda: C.sparse_decompress(rows, ys, prob_bits=pb, ws=ws))
+        record(f"c4: {nbs} x 15M fp32, 90 % zeros (sparse bitmap + dense codec)", nbs * 15000000 * 4,
+               int(sizes.to(torch.int64).sum()), tc, td, exact, kernels_ms=kern)
+        del fs, ys, arch, rows
     return out
 
 

@@ -195,6 +195,10 @@ uint32_t deviceErrorCount(bool reset) {
 // formats without a caller-supplied histogram, elements of at most
 // pc::kMaxTeam items (1 MiB of symbols).  One generation of resident
 // workgroups pulls items off the work queue.
+bool persistentFits(uint32_t maxWords) {
+  return divUp(divUp(maxWords, kBlockSize), pc::kBlocksPerItem) <= pc::kMaxTeam;
+}
+
 template <int FT, bool kCk>
 bool compressPersistent(StackDeviceMemory& res, int pb, bool useChecksum, uint32_t nb,
                         const BatchDesc& in, uint32_t maxSize, const BatchDesc& out,
@@ -231,7 +235,7 @@ bool compressPersistent(StackDeviceMemory& res, int pb, bool useChecksum, uint32
   const uint32_t teams = grid / team;
   const uint32_t maxR = 2 * divUp(nb, teams) + 2;
   const size_t regions[kSyncRegions] = {16, size_t(items) * 8, partBytes + (kCk ? size_t(items) * 4 : 0),
-                                        size_t(teams) * maxR * 8};
+                                        size_t(teams) * maxR * 8, 0};
   SyncLease lease(res, s, regions);
   if (FT != 0 && useChecksum) {
     HIP_CHECK(hipMemsetAsync(ck.data(), 0, sizeof(uint32_t) * nb, s));
@@ -280,16 +284,17 @@ template <int FT>
 void encodeBatchDevice(StackDeviceMemory& res, int pb, bool useChecksum, uint32_t nb,
                        const BatchDesc& inArg, uint32_t maxSize, const uint32_t* hist_dev,
                        const BatchDesc& outArg, uint32_t* outSize_dev, hipStream_t s,
-                       const DeviceTables* tabs, bool inAligned16) {
+                       const DeviceTables* tabs, bool inAligned16, const PartialHist* pre = nullptr) {
   checkProbBits(pb);
   if (nb == 0) return;
   constexpr int kSegs = FloatTraits<FT>::kSegs;
   constexpr bool kFused = kSegs == 1;  // k_encode writes the archive itself
   const uint32_t MB = divUp(maxSize, kBlockSize);
-  const uint32_t chunkWords = histChunkWords(nb, maxSize);
-  const uint32_t chunks = std::max(1u, divUp(maxSize, chunkWords));
   const bool userHist = FT == 0 && hist_dev != nullptr;
-  const bool runHist = !userHist || useChecksum;
+  const bool preHist = FT != 0 && pre != nullptr;  // partial rows counted by the caller
+  const uint32_t chunkWords = histChunkWords(nb, maxSize);
+  const uint32_t chunks = preHist ? std::max(1u, pre->nRows) : std::max(1u, divUp(maxSize, chunkWords));
+  const bool runHist = !preHist && (!userHist || useChecksum);
   const bool rawCk = FT == 0 && useChecksum;
   if constexpr (kFused) {
     if (!userHist && inAligned16) {
@@ -306,9 +311,10 @@ void encodeBatchDevice(StackDeviceMemory& res, int pb, bool useChecksum, uint32_
 
   auto partHist = res.alloc<uint32_t>(s, runHist ? size_t(kSegs) * nb * chunks * kNumSymbols : 1);
   auto partCk = res.alloc<uint32_t>(s, rawCk ? size_t(nb) * chunks : 1);
+  const uint32_t* chunkRows = preHist ? pre->rows : partHist.data();
   // first-level sums when elements have many chunks (k_histReduce)
   const uint32_t groups = divUp(chunks, kReduceRows);
-  const bool reduce2 = runHist && chunks > kReduceRows;
+  const bool reduce2 = (runHist || preHist) && chunks > kReduceRows;
   auto groupHist = res.alloc<uint32_t>(s, reduce2 ? size_t(kSegs) * nb * groups * kNumSymbols : 1);
   auto groupCk = res.alloc<uint32_t>(s, reduce2 && rawCk ? size_t(nb) * groups : 1);
   auto ck = res.alloc<uint32_t>(s, nb);
@@ -318,6 +324,31 @@ void encodeBatchDevice(StackDeviceMemory& res, int pb, bool useChecksum, uint32_
   auto cw = res.alloc<uint32_t>(s, kFused ? 1 : size_t(kSegs) * nb * std::max(MB, 1u));
   const uint32_t nW = std::max(1u, divUp(MB, EncCfg<FT>::kBlocksPerWG));
   auto flags = res.alloc<uint64_t>(s, kFused ? size_t(nb) * nW : 1);
+  // the normalisation runs in the last workgroup of the kernel that writes
+  // an element's final partial rows (k_histReduce, or a k_hist of at most
+  // 4096 workgroups), saving the k_normalize launch.  Each of those
+  // workgroups pays a wait for its rows' write-through stores and a counter
+  // round trip: with many (c3's k_hist: 65,536) that costs more than the
+  // launch (c3 hist 0.74 -> 1.09 ms), so k_normalize runs there.
+  const bool finalInReduce = reduce2;
+  const bool finalInHist = !reduce2 && runHist && uint64_t(chunks) * nb <= 4096;
+  const size_t regions[kSyncRegions] = {0, 0, 0, 0, size_t(nb) * 4};
+  SyncLease lease(res, s, regions);
+  NormArgs na;
+  na.in = in;
+  na.hist = userHist ? hist_dev : (reduce2 ? groupHist.data() : chunkRows);
+  na.rows = userHist ? 1u : (reduce2 ? groups : chunks);
+  na.pb = pb;
+  na.table = table.data();
+  na.pdf = pdf.data();
+  na.partCk = rawCk ? (reduce2 ? groupCk.data() : partCk.data()) : nullptr;
+  na.ckRows = reduce2 ? groups : chunks;
+  na.ckOut = ck.data();
+  na.flags = kFused ? flags.data() : nullptr;
+  na.nW = nW;
+  na.arrive = nullptr;
+  NormArgs naFinal = na;
+  naFinal.arrive = static_cast<uint32_t*>(lease.base[kSyncArrive]);
 
   if (FT != 0 && useChecksum) {
     HIP_CHECK(hipMemsetAsync(ck.data(), 0, sizeof(uint32_t) * nb, s));
@@ -327,12 +358,13 @@ void encodeBatchDevice(StackDeviceMemory& res, int pb, bool useChecksum, uint32_
     if (runHist) {
       prof::Scope p("hist", s);
       dim3 g(chunks, ny);
+      const NormArgs& nh = finalInHist ? naFinal : na;
       if (rawCk) {
         k_hist<FT, true><<<g, kThreads, 0, s>>>(in, y0, nb, chunkWords, chunks, partHist.data(),
-                                                partCk.data());
+                                                partCk.data(), nh);
       } else {
         k_hist<FT, false><<<g, kThreads, 0, s>>>(in, y0, nb, chunkWords, chunks, partHist.data(),
-                                                 nullptr);
+                                                 nullptr, nh);
       }
       HIP_LAUNCH_CHECK();
     }
@@ -344,30 +376,18 @@ void encodeBatchDevice(StackDeviceMemory& res, int pb, bool useChecksum, uint32_
       k_checksum<<<g, kThreads, 0, s>>>(in, y0, 1, ckChunk, ck.data());
       HIP_LAUNCH_CHECK();
     }
-    const uint32_t* histRows = userHist ? hist_dev : partHist.data();
-    const uint32_t* ckRows = rawCk ? partCk.data() : nullptr;
-    uint32_t nHistRows = userHist ? 1u : chunks, nCkRows = chunks;
     if (reduce2) {
       prof::Scope p("normalize", s);
       dim3 g(groups, ny, kSegs);
-      k_histReduce<<<g, kThreads, 0, s>>>(y0, nb, chunks, groups, partHist.data(), ckRows,
-                                          groupHist.data(), rawCk ? groupCk.data() : nullptr);
+      k_histReduce<<<g, kThreads, 0, s>>>(y0, nb, chunks, groups, chunkRows, rawCk ? partCk.data() : nullptr,
+                                          groupHist.data(), rawCk ? groupCk.data() : nullptr,
+                                          finalInReduce ? naFinal : na, kSegs);
       HIP_LAUNCH_CHECK();
-      if (!userHist) {
-        histRows = groupHist.data();
-        nHistRows = groups;
-      }
-      if (rawCk) {
-        ckRows = groupCk.data();
-        nCkRows = groups;
-      }
     }
-    {
+    if (!finalInReduce && !finalInHist) {
       prof::Scope p("normalize", s);
       dim3 g(ny, kSegs);
-      k_normalize<<<g, kThreads, 0, s>>>(in, y0, nb, histRows, nHistRows, pb, table.data(),
-                                         pdf.data(), ckRows, nCkRows, ck.data(),
-                                         kFused ? flags.data() : nullptr, nW);
+      k_normalize<<<g, kThreads, 0, s>>>(na, y0, nb);
       HIP_LAUNCH_CHECK();
     }
     if (MB > 0 || kFused) {
@@ -684,25 +704,25 @@ static void checkFloatConfig(const FloatCodecConfig& c) {
 void floatCompressDescs(StackDeviceMemory& res, const FloatCompressConfig& config, uint32_t nb,
                         const BatchDesc& in, uint32_t maxSize, const BatchDesc& out,
                         uint32_t* outSize_dev, hipStream_t s, const DeviceTables* tabs,
-                        bool inAligned16) {
+                        bool inAligned16, const PartialHist* pre) {
   checkFloatConfig(config);
   const int pb = config.ansConfig.probBits;
   switch (config.floatType) {
     case FloatType::kFloat16:
       encodeBatchDevice<1>(res, pb, config.useChecksum, nb, in, maxSize, nullptr, out, outSize_dev, s,
-                             tabs, inAligned16);
+                             tabs, inAligned16, pre);
       break;
     case FloatType::kBFloat16:
       encodeBatchDevice<2>(res, pb, config.useChecksum, nb, in, maxSize, nullptr, out, outSize_dev, s,
-                             tabs, inAligned16);
+                             tabs, inAligned16, pre);
       break;
     case FloatType::kFloat32:
       encodeBatchDevice<3>(res, pb, config.useChecksum, nb, in, maxSize, nullptr, out, outSize_dev, s,
-                             tabs, inAligned16);
+                             tabs, inAligned16, pre);
       break;
     default:
       encodeBatchDevice<4>(res, pb, config.useChecksum, nb, in, maxSize, nullptr, out, outSize_dev, s,
-                             tabs, inAligned16);
+                             tabs, inAligned16, pre);
       break;
   }
 }

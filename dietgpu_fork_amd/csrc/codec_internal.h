@@ -12,10 +12,23 @@ namespace dietgpu {
 
 struct DeviceTables;  // codec.hip: per-call pointer tables (maybe kernel-argument inline)
 
+// Partial symbol histograms of the float words counted by the caller (the
+// sparse compressor counts its nonzeros as it compacts them, so the dense
+// codec's histogram pass is skipped): u32 rows [segments][nb][nRows][256],
+// summed per element.  Ignored when the single-pass compressor takes the call.
+struct PartialHist {
+  const uint32_t* rows;
+  uint32_t nRows;
+};
+
 void floatCompressDescs(StackDeviceMemory& res, const FloatCompressConfig& config, uint32_t nb,
                         const BatchDesc& in, uint32_t maxSize, const BatchDesc& out,
                         uint32_t* outSize_dev, hipStream_t s, const DeviceTables* tabs = nullptr,
-                        bool inAligned16 = false);
+                        bool inAligned16 = false, const PartialHist* pre = nullptr);
+
+// The single-pass compressor (k_pcompress) takes float elements of at most
+// this many words (and 16 B-aligned inputs).
+bool persistentFits(uint32_t maxWords);
 
 FloatDecompressStatus floatDecompressDescs(StackDeviceMemory& res,
                                            const FloatDecompressConfig& config, uint32_t nb,

@@ -207,4 +207,21 @@ __device__ __forceinline__ void buildLut(gp<const uint16_t> pdfIn, uint32_t* lut
   }
 }
 
+// sc1 (agent-scope relaxed) loads / stores: the cross-workgroup hand-offs'
+// accesses (MI355X_MICROARCH.md, sc1 loads in place of an acquire)
+__device__ __forceinline__ uint32_t ldSc1(gp<const uint32_t> p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// four consecutive words as two 8 B sc1 loads (each word carries its own tag,
+// so the two halves need not be read at one instant)
+__device__ __forceinline__ u32x4 ldSc1x4(gp<const u32x4> p) {
+  gp<const uint64_t> q = (gp<const uint64_t>)p;
+  const uint64_t a = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint64_t b = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return u32x4{uint32_t(a), uint32_t(a >> 32), uint32_t(b), uint32_t(b >> 32)};
+}
+__device__ __forceinline__ void stSc1(gp<uint32_t> p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 }  // namespace dietgpu

@@ -24,160 +24,6 @@ constexpr int kThreads = 256;
 constexpr int kWaves = kThreads / 64;
 constexpr uint32_t kSlotBytes = kStateBytesPerBlock + kSlotDataBytes;
 
-// ---------------------------------------------------------------------------
-// k_hist: per-chunk symbol histogram(s) (+ byte-XOR checksum for raw bytes).
-// grid (chunksPerElem, batch).  Each workgroup writes its 256 (x segs)
-// partial counts without atomics; k_normalize sums them.  LDS counters are
-// laid out bin-major with one column per lane of a 32-lane group
-// (hs[sym * 32 + (lane & 31)]): every ds_add of a wave half hits 32
-// distinct banks and never the same address, however skewed the symbol
-// distribution (float exponents concentrate on a handful of values).
-// ---------------------------------------------------------------------------
-constexpr int kHistCols = 32;
-
-template <int FT, bool kChecksum>
-__global__ __launch_bounds__(kThreads) void k_hist(BatchDesc in, uint32_t batchOffset,
-                                                   uint32_t numInBatch, uint32_t chunkWords,
-                                                   uint32_t chunksPerElem,
-                                                   uint32_t* __restrict__ partHist,
-                                                   uint32_t* __restrict__ partCk) {
-  using WordT = typename FloatTraits<FT>::WordT;
-  constexpr int kSegs = FloatTraits<FT>::kSegs;
-  __shared__ __attribute__((aligned(16))) uint32_t hs[kSegs][kNumSymbols * kHistCols];
-  __shared__ uint32_t red[kWaves];
-
-  const uint32_t b = batchOffset + blockIdx.y;
-  const uint32_t c = blockIdx.x;
-  const uint32_t tid = threadIdx.x;
-  for (int s = 0; s < kSegs; ++s)
-    for (uint32_t i = tid; i < kNumSymbols * kHistCols / 4; i += kThreads)
-      *(lp<u32x4>)&hs[s][4 * i] = u32x4{0, 0, 0, 0};
-  __syncthreads();
-
-  const uint32_t size = in.size(b);
-  const uint64_t begin = uint64_t(c) * chunkWords;
-  uint32_t ck = 0;
-  uint32_t* h0 = &hs[0][tid & (kHistCols - 1)];
-  uint32_t* h1 = &hs[kSegs - 1][tid & (kHistCols - 1)];
-  auto addWord = [&](WordT w) {
-    atomicAdd(&h0[compOf<FT>(w, 0) * kHistCols], 1u);
-    if constexpr (kSegs == 2) atomicAdd(&h1[compOf<FT>(w, 1) * kHistCols], 1u);
-  };
-
-  if (begin < size) {
-    const uint32_t n = uint32_t(min(uint64_t(chunkWords), uint64_t(size) - begin));
-    gp<const WordT> q = (gp<const WordT>)startOf(in, b) + begin;
-    constexpr uint32_t kPerVec = 16 / sizeof(WordT);
-    const uintptr_t qa = reinterpret_cast<uintptr_t>(q);
-    uint32_t head = uint32_t(((16 - (qa & 15)) & 15) / sizeof(WordT));
-    if ((qa & (sizeof(WordT) - 1)) != 0) head = n;
-    head = min(head, n);
-    for (uint32_t i = tid; i < head; i += kThreads) {
-      const WordT w = q[i];
-      addWord(w);
-      if constexpr (kChecksum) ck ^= uint32_t(w);
-    }
-    gp<const uint4> q4 = (gp<const uint4>)(q + head);
-    const uint32_t n4 = (n - head) / kPerVec;
-    // software-pipelined main part: the next 4-vector batch is in flight
-    // while the current one is counted (uniform trip count, so the loads
-    // are unconditional and each wait is a counted vmcnt)
-    constexpr uint32_t kB = 4 * kThreads;
-    const uint32_t nIt = n4 / kB;
-    uint32_t i = tid;
-    auto count4 = [&](const uint4 (&v)[4]) {
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const WordT* ws = reinterpret_cast<const WordT*>(&v[k]);
-#pragma unroll
-        for (uint32_t j = 0; j < kPerVec; ++j) addWord(ws[j]);
-        if constexpr (kChecksum) ck ^= v[k].x ^ v[k].y ^ v[k].z ^ v[k].w;
-      }
-    };
-    if (nIt > 0) {
-      uint4 cur[4];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) cur[k] = ld16(q4 + i + k * kThreads);
-      for (uint32_t it = 1; it < nIt; ++it) {
-        uint4 nxt[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) nxt[k] = ld16(q4 + i + kB + k * kThreads);
-        count4(cur);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) cur[k] = nxt[k];
-        i += kB;
-      }
-      count4(cur);
-      i += kB;
-    }
-    for (; i < n4; i += kThreads) {
-      const uint4 v = ld16(q4 + i);
-      const WordT* ws = reinterpret_cast<const WordT*>(&v);
-#pragma unroll
-      for (uint32_t j = 0; j < kPerVec; ++j) addWord(ws[j]);
-      if constexpr (kChecksum) ck ^= v.x ^ v.y ^ v.z ^ v.w;
-    }
-    for (uint32_t t = head + n4 * kPerVec + tid; t < n; t += kThreads) {
-      const WordT w = q[t];
-      addWord(w);
-      if constexpr (kChecksum) ck ^= uint32_t(w);
-    }
-  }
-  __syncthreads();
-  for (int s = 0; s < kSegs; ++s) {
-    // bin tid: sum its 32 columns, rotated so the wave's reads spread banks
-    uint32_t sum = 0;
-#pragma unroll
-    for (int k = 0; k < kHistCols; ++k) sum += hs[s][tid * kHistCols + ((k + tid) & (kHistCols - 1))];
-    G(partHist)[((uint64_t(s) * numInBatch + b) * chunksPerElem + c) * kNumSymbols + tid] = sum;
-  }
-  if constexpr (kChecksum) {
-    ck = (ck ^ (ck >> 8) ^ (ck >> 16) ^ (ck >> 24)) & 0xffu;
-    ck = waveXor(ck);
-    if ((tid & 63) == 0) red[tid >> 6] = ck;
-    __syncthreads();
-    if (tid == 0) G(partCk)[uint64_t(b) * chunksPerElem + c] = red[0] ^ red[1] ^ red[2] ^ red[3];
-  }
-}
-
-// ---------------------------------------------------------------------------
-// k_histReduce: first level of the partial-histogram sum when an element has
-// many chunks (few large elements: one 128 MiB fp64 tensor is 2048 chunks,
-// which k_normalize's single workgroup would sum serially for ~0.3 ms).
-// grid (groups, batch, segments): workgroup g sums chunks [64g, 64g + 64) of
-// its (element, segment) row, and the byte-checksum partials likewise.
-// ---------------------------------------------------------------------------
-constexpr uint32_t kReduceRows = 64;
-
-static __global__ __launch_bounds__(kThreads) void k_histReduce(
-    uint32_t batchOffset, uint32_t numInBatch, uint32_t chunksPerElem, uint32_t groups,
-    const uint32_t* __restrict__ part, const uint32_t* __restrict__ partCk,
-    uint32_t* __restrict__ outHist, uint32_t* __restrict__ outCk) {
-  const uint32_t b = batchOffset + blockIdx.y;
-  const uint32_t g = blockIdx.x;
-  const uint64_t row = uint64_t(blockIdx.z) * numInBatch + b;
-  const uint32_t c0 = g * kReduceRows;
-  const uint32_t c1 = min(chunksPerElem, c0 + kReduceRows);
-  gp<const uint32_t> hp = G(part) + (row * chunksPerElem) * kNumSymbols + threadIdx.x;
-  uint32_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  uint32_t c = c0;
-  for (; c + 8 <= c1; c += 8) {
-#pragma unroll
-    for (int k = 0; k < 8; ++k) acc[k] += hp[uint64_t(c + k) * kNumSymbols];
-  }
-  for (; c < c1; ++c) acc[0] += hp[uint64_t(c) * kNumSymbols];
-  uint32_t sum = 0;
-#pragma unroll
-  for (int k = 0; k < 8; ++k) sum += acc[k];
-  G(outHist)[(row * groups + g) * kNumSymbols + threadIdx.x] = sum;
-  if (partCk && blockIdx.z == 0 && threadIdx.x < 64) {
-    uint32_t ck = 0;
-    for (uint32_t k = c0 + threadIdx.x; k < c1; k += 64) ck ^= G(partCk)[uint64_t(b) * chunksPerElem + k];
-    ck = waveXor(ck);
-    if (threadIdx.x == 0) G(outCk)[uint64_t(b) * groups + g] = ck;
-  }
-}
-
 // Bit-exact restatement of normalizeProbabilitiesFromHistogram
 // (ans/GpuANSStatistics.cuh:178-366) for one kThreads-thread workgroup, thread
 // s = symbol s: float32 quantisation, descending order of the unique keys
@@ -361,44 +207,290 @@ __device__ __forceinline__ uint4 encTableEntryReg(uint32_t q, uint32_t cdf, int 
 }
 
 // ---------------------------------------------------------------------------
-// k_normalize: one workgroup per (element, segment): sums the partial
-// histograms, normalises (normalizeCount) and stores the encode table rows
-// (encTableEntry) and the u16 pdf.
+// Normalisation of one (element, segment): sums the partial histograms,
+// normalises (normalizeCount) and stores the encode table rows
+// (encTableEntry) and the u16 pdf.  Run by k_normalize, or -- one launch
+// fewer -- by the last workgroup to finish an element in the kernel that
+// writes its final partial rows (k_hist or k_histReduce: NormArgs::arrive,
+// the classic last-block reduction: every workgroup counts itself in after
+// a release fence; the one that takes the count to its total, having
+// acquired, sees every row).
 // ---------------------------------------------------------------------------
-static __global__ __launch_bounds__(kThreads) void k_normalize(
-    BatchDesc in, uint32_t batchOffset, uint32_t numInBatch, const uint32_t* __restrict__ hist,
-    uint32_t chunksPerElem, int pb, uint4* __restrict__ table, uint16_t* __restrict__ pdfOut,
-    const uint32_t* __restrict__ partCk, uint32_t ckChunks, uint32_t* __restrict__ ckOut,
-    uint64_t* __restrict__ flags, uint32_t nW) {
-  __shared__ uint32_t keys[kNumSymbols];
-  __shared__ uint32_t red[kWaves];
-  const uint32_t b = batchOffset + blockIdx.x;
-  const uint32_t seg = blockIdx.y;
+// Column sums of `rows` rows of 256 u32 (row stride 256) by one workgroup:
+// thread t loads 16 B (bins 4(t & 63) .. +3) of every fourth row (rows
+// congruent to t >> 6), eight rows in flight, and the four row streams meet
+// in LDS (`red4`: 256 x 16 B).  Returns bin t's sum.  A row per thread
+// per load would expose one memory round trip per eight rows; this takes
+// one per 32.
+// kSc1: the rows were handed off inside this launch (sc1 stores, last
+// arrival): every load of them is an sc1 load.
+template <bool kSc1>
+__device__ __forceinline__ uint32_t sumRows256(gp<const uint32_t> base, uint32_t rows, u32x4* red4) {
+  const uint32_t t = threadIdx.x, q = t & 63, st = t >> 6;
+  gp<const u32x4> p = (gp<const u32x4>)base + q;
+  auto ld = [&](uint32_t r) { return kSc1 ? ldSc1x4(p + uint64_t(r) * (kNumSymbols / 4)) : p[uint64_t(r) * (kNumSymbols / 4)]; };
+  u32x4 acc[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) acc[k] = u32x4{0, 0, 0, 0};
+  uint32_t r = st;
+  for (; r + 28 < rows; r += 32) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc[k] += ld(r + 4 * k);
+  }
+  for (; r < rows; r += 4) acc[0] += ld(r);
+#pragma unroll
+  for (int k = 1; k < 8; ++k) acc[0] += acc[k];
+  __syncthreads();  // red4 free
+  red4[st * 64 + q] = acc[0];
+  __syncthreads();
+  const uint32_t qq = t >> 2, j = t & 3;
+  uint32_t sum = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < 4; ++k) {
+    const u32x4 v = red4[k * 64 + qq];
+    sum += j == 0 ? v.x : j == 1 ? v.y : j == 2 ? v.z : v.w;
+  }
+  __syncthreads();  // red4 reusable
+  return sum;
+}
+
+struct NormArgs {
+  BatchDesc in;                 // symbol totals (element sizes)
+  const uint32_t* hist;         // [segs][nb][rows][256] rows to sum
+  uint32_t rows;
+  int pb;
+  uint4* table;                 // [segs][nb][256]
+  uint16_t* pdf;                // [segs][nb][256]
+  const uint32_t* partCk;       // [nb][ckRows] byte-checksum partials, or null
+  uint32_t ckRows;
+  uint32_t* ckOut;
+  uint64_t* flags;              // k_encode's look-back flags ([nb][nW]), or null
+  uint32_t nW;
+  uint32_t* arrive;             // [nb] last-arrival counters (self-resetting), or null
+};
+
+__device__ __forceinline__ void normalizeElement(const NormArgs& a, uint32_t numInBatch, uint32_t b,
+                                                 uint32_t seg, uint32_t* keys, uint32_t* red, u32x4* red4) {
   const uint32_t s = threadIdx.x;
   const uint64_t row = uint64_t(seg) * numInBatch + b;
-  if (flags && seg == 0)  // k_encode's look-back flags (EncTail)
-    for (uint32_t i = s; i < nW; i += kThreads) G(flags)[uint64_t(b) * nW + i] = 0;
-
-  if (partCk && seg == 0 && s == 0) {
+  if (a.flags && seg == 0)  // k_encode's look-back flags (EncTail)
+    for (uint32_t i = s; i < a.nW; i += kThreads) G(a.flags)[uint64_t(b) * a.nW + i] = 0;
+  // (arrive set: the last arrival of this launch, rows and checksum
+  // partials handed off with sc1 stores, read with sc1 loads)
+  const bool sc1 = a.arrive != nullptr;
+  if (a.partCk && seg == 0 && s == 0) {
     uint32_t ck = 0;
-    for (uint32_t c = 0; c < ckChunks; ++c) ck ^= G(partCk)[uint64_t(b) * ckChunks + c];
-    G(ckOut)[b] = ck;
+    for (uint32_t c = 0; c < a.ckRows; ++c) {
+      gp<const uint32_t> pc = G(a.partCk) + uint64_t(b) * a.ckRows + c;
+      ck ^= sc1 ? ldSc1(pc) : *pc;
+    }
+    G(a.ckOut)[b] = ck;
   }
-  uint32_t count = 0;
-  gp<const uint32_t> hp = G(hist) + row * chunksPerElem * kNumSymbols + s;
-#pragma unroll 8
-  for (uint32_t c = 0; c < chunksPerElem; ++c) count += hp[uint64_t(c) * kNumSymbols];
+  gp<const uint32_t> rowsBase = G(a.hist) + row * a.rows * kNumSymbols;
+  const uint32_t count = sc1 ? sumRows256<true>(rowsBase, a.rows, red4) : sumRows256<false>(rowsBase, a.rows, red4);
 
-  const uint32_t total = in.size(b);
+  const uint32_t total = a.in.size(b);
   if (total == 0) {  // :193-195 (the reference leaves the table untouched)
-    st16(G(table) + row * kNumSymbols + s, make_uint4(0, 0, 0, 0));
-    G(pdfOut)[row * kNumSymbols + s] = 0;
+    st16(G(a.table) + row * kNumSymbols + s, make_uint4(0, 0, 0, 0));
+    G(a.pdf)[row * kNumSymbols + s] = 0;
     return;
   }
-  const uint32_t q = normalizeCount(count, total, pb, keys, red);
+  const uint32_t q = normalizeCount(count, total, a.pb, keys, red);
   const uint32_t cdf = blockExclusiveScan<kThreads>(q, red, nullptr);
-  st16(G(table) + row * kNumSymbols + s, encTableEntry(q, cdf, pb));
-  G(pdfOut)[row * kNumSymbols + s] = uint16_t(q);
+  st16(G(a.table) + row * kNumSymbols + s, encTableEntry(q, cdf, a.pb));
+  G(a.pdf)[row * kNumSymbols + s] = uint16_t(q);
+}
+
+// After this workgroup's rows of element b are stored -- with sc1 stores --
+// true in the one workgroup that completes the element's `arrivals`.  The
+// hand-off is MI355X_MICROARCH.md's counter form without fences: every
+// storing wave waits for its sc1 stores, a barrier, then one lane's counter
+// add; the last arrival reads the rows with sc1 loads only (an agent fence
+// per workgroup writes back and invalidates the XCD's L2: 3.5 us each, c3's
+// 1024 workgroups took 15 ms).  The counter wraps to 0 on the last arrival,
+// ready for the next call.  Whole workgroup; `flag`: one LDS word.
+__device__ __forceinline__ bool lastArrival(uint32_t* counter, uint32_t arrivals, uint32_t* flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's sc1 row stores are done
+  __syncthreads();
+  if (threadIdx.x == 0) *flag = atomicInc(counter, arrivals - 1) == arrivals - 1 ? 1u : 0u;
+  __syncthreads();
+  return *flag != 0;
+}
+
+static __global__ __launch_bounds__(kThreads) void k_normalize(NormArgs a, uint32_t batchOffset,
+                                                               uint32_t numInBatch) {
+  __shared__ uint32_t keys[kNumSymbols];
+  __shared__ uint32_t red[kWaves];
+  __shared__ u32x4 red4[kThreads];
+  normalizeElement(a, numInBatch, batchOffset + blockIdx.x, blockIdx.y, keys, red, red4);
+}
+
+// ---------------------------------------------------------------------------
+// k_hist: per-chunk symbol histogram(s) (+ byte-XOR checksum for raw bytes).
+// grid (chunksPerElem, batch).  Each workgroup writes its 256 (x segs)
+// partial counts without atomics; k_normalize sums them.  LDS counters are
+// laid out bin-major with one column per lane of a 32-lane group
+// (hs[sym * 32 + (lane & 31)]): every ds_add of a wave half hits 32
+// distinct banks and never the same address, however skewed the symbol
+// distribution (float exponents concentrate on a handful of values).
+// ---------------------------------------------------------------------------
+constexpr int kHistCols = 32;
+
+template <int FT, bool kChecksum>
+__global__ __launch_bounds__(kThreads) void k_hist(BatchDesc in, uint32_t batchOffset,
+                                                   uint32_t numInBatch, uint32_t chunkWords,
+                                                   uint32_t chunksPerElem,
+                                                   uint32_t* __restrict__ partHist,
+                                                   uint32_t* __restrict__ partCk, NormArgs na) {
+  using WordT = typename FloatTraits<FT>::WordT;
+  constexpr int kSegs = FloatTraits<FT>::kSegs;
+  __shared__ __attribute__((aligned(16))) uint32_t hs[kSegs][kNumSymbols * kHistCols];
+  __shared__ uint32_t red[kWaves];
+
+  const uint32_t b = batchOffset + blockIdx.y;
+  const uint32_t c = blockIdx.x;
+  const uint32_t tid = threadIdx.x;
+  for (int s = 0; s < kSegs; ++s)
+    for (uint32_t i = tid; i < kNumSymbols * kHistCols / 4; i += kThreads)
+      *(lp<u32x4>)&hs[s][4 * i] = u32x4{0, 0, 0, 0};
+  __syncthreads();
+
+  const uint32_t size = in.size(b);
+  const uint64_t begin = uint64_t(c) * chunkWords;
+  uint32_t ck = 0;
+  uint32_t* h0 = &hs[0][tid & (kHistCols - 1)];
+  uint32_t* h1 = &hs[kSegs - 1][tid & (kHistCols - 1)];
+  auto addWord = [&](WordT w) {
+    atomicAdd(&h0[compOf<FT>(w, 0) * kHistCols], 1u);
+    if constexpr (kSegs == 2) atomicAdd(&h1[compOf<FT>(w, 1) * kHistCols], 1u);
+  };
+
+  if (begin < size) {
+    const uint32_t n = uint32_t(min(uint64_t(chunkWords), uint64_t(size) - begin));
+    gp<const WordT> q = (gp<const WordT>)startOf(in, b) + begin;
+    constexpr uint32_t kPerVec = 16 / sizeof(WordT);
+    const uintptr_t qa = reinterpret_cast<uintptr_t>(q);
+    uint32_t head = uint32_t(((16 - (qa & 15)) & 15) / sizeof(WordT));
+    if ((qa & (sizeof(WordT) - 1)) != 0) head = n;
+    head = min(head, n);
+    for (uint32_t i = tid; i < head; i += kThreads) {
+      const WordT w = q[i];
+      addWord(w);
+      if constexpr (kChecksum) ck ^= uint32_t(w);
+    }
+    gp<const uint4> q4 = (gp<const uint4>)(q + head);
+    const uint32_t n4 = (n - head) / kPerVec;
+    // software-pipelined main part: the next 4-vector batch is in flight
+    // while the current one is counted (uniform trip count, so the loads
+    // are unconditional and each wait is a counted vmcnt)
+    constexpr uint32_t kB = 4 * kThreads;
+    const uint32_t nIt = n4 / kB;
+    uint32_t i = tid;
+    auto count4 = [&](const uint4 (&v)[4]) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const WordT* ws = reinterpret_cast<const WordT*>(&v[k]);
+#pragma unroll
+        for (uint32_t j = 0; j < kPerVec; ++j) addWord(ws[j]);
+        if constexpr (kChecksum) ck ^= v[k].x ^ v[k].y ^ v[k].z ^ v[k].w;
+      }
+    };
+    if (nIt > 0) {
+      uint4 cur[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) cur[k] = ld16(q4 + i + k * kThreads);
+      for (uint32_t it = 1; it < nIt; ++it) {
+        uint4 nxt[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) nxt[k] = ld16(q4 + i + kB + k * kThreads);
+        count4(cur);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) cur[k] = nxt[k];
+        i += kB;
+      }
+      count4(cur);
+      i += kB;
+    }
+    for (; i < n4; i += kThreads) {
+      const uint4 v = ld16(q4 + i);
+      const WordT* ws = reinterpret_cast<const WordT*>(&v);
+#pragma unroll
+      for (uint32_t j = 0; j < kPerVec; ++j) addWord(ws[j]);
+      if constexpr (kChecksum) ck ^= v.x ^ v.y ^ v.z ^ v.w;
+    }
+    for (uint32_t t = head + n4 * kPerVec + tid; t < n; t += kThreads) {
+      const WordT w = q[t];
+      addWord(w);
+      if constexpr (kChecksum) ck ^= uint32_t(w);
+    }
+  }
+  __syncthreads();
+  for (int s = 0; s < kSegs; ++s) {
+    // bin tid: sum its 32 columns, rotated so the wave's reads spread banks
+    uint32_t sum = 0;
+#pragma unroll
+    for (int k = 0; k < kHistCols; ++k) sum += hs[s][tid * kHistCols + ((k + tid) & (kHistCols - 1))];
+    gp<uint32_t> dst = G(partHist) + ((uint64_t(s) * numInBatch + b) * chunksPerElem + c) * kNumSymbols + tid;
+    if (na.arrive) stSc1(dst, sum);  // read by this launch's last arrival
+    else *dst = sum;
+  }
+  if constexpr (kChecksum) {
+    ck = (ck ^ (ck >> 8) ^ (ck >> 16) ^ (ck >> 24)) & 0xffu;
+    ck = waveXor(ck);
+    if ((tid & 63) == 0) red[tid >> 6] = ck;
+    __syncthreads();
+    if (tid == 0) {
+      gp<uint32_t> dst = G(partCk) + uint64_t(b) * chunksPerElem + c;
+      if (na.arrive) stSc1(dst, red[0] ^ red[1] ^ red[2] ^ red[3]);
+      else *dst = red[0] ^ red[1] ^ red[2] ^ red[3];
+    }
+  }
+  // the element's last workgroup normalises it (hs is free: keys there)
+  if (na.arrive && lastArrival(na.arrive + b, chunksPerElem, &red[0])) {
+    for (int s = 0; s < kSegs; ++s) {
+      normalizeElement(na, numInBatch, b, s, &hs[0][0], &hs[0][kNumSymbols],
+                       reinterpret_cast<u32x4*>(&hs[0][2 * kNumSymbols]));
+      __syncthreads();
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// k_histReduce: first level of the partial-histogram sum when an element has
+// many chunks (few large elements: one 128 MiB fp64 tensor is 2048 chunks,
+// which k_normalize's single workgroup would sum serially for ~0.3 ms).
+// grid (groups, batch, segments): workgroup g sums chunks [64g, 64g + 64) of
+// its (element, segment) row, and the byte-checksum partials likewise.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kReduceRows = 64;
+
+static __global__ __launch_bounds__(kThreads) void k_histReduce(
+    uint32_t batchOffset, uint32_t numInBatch, uint32_t chunksPerElem, uint32_t groups,
+    const uint32_t* __restrict__ part, const uint32_t* __restrict__ partCk,
+    uint32_t* __restrict__ outHist, uint32_t* __restrict__ outCk, NormArgs na, uint32_t segs) {
+  __shared__ uint32_t keys[kNumSymbols];
+  __shared__ uint32_t red[kWaves + 1];
+  __shared__ u32x4 red4[kThreads];
+  const uint32_t b = batchOffset + blockIdx.y;
+  const uint32_t g = blockIdx.x;
+  const uint64_t row = uint64_t(blockIdx.z) * numInBatch + b;
+  const uint32_t c0 = g * kReduceRows;
+  const uint32_t c1 = min(chunksPerElem, c0 + kReduceRows);
+  const uint32_t sum = sumRows256<false>(G(part) + (row * chunksPerElem + c0) * kNumSymbols, c1 - c0, red4);
+  stSc1(G(outHist) + (row * groups + g) * kNumSymbols + threadIdx.x, sum);
+  if (partCk && blockIdx.z == 0 && threadIdx.x < 64) {
+    uint32_t ck = 0;
+    for (uint32_t k = c0 + threadIdx.x; k < c1; k += 64) ck ^= G(partCk)[uint64_t(b) * chunksPerElem + k];
+    ck = waveXor(ck);
+    if (threadIdx.x == 0) stSc1(G(outCk) + uint64_t(b) * groups + g, ck);
+  }
+  // the element's last workgroup (over groups and segments) normalises it
+  if (na.arrive && lastArrival(na.arrive + b, groups * segs, &red[kWaves])) {
+    for (uint32_t s = 0; s < segs; ++s) {
+      normalizeElement(na, numInBatch, b, s, keys, red, red4);
+      __syncthreads();
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------

@@ -83,15 +83,29 @@ __device__ __forceinline__ void loadTile(gp<const W> x, uint32_t t0, uint32_t ti
 // flags is the step's 64 bitmap bits (generate_bitmap :40-71) and its
 // nonzeros' ranks (v_mbcnt).  The nonzeros go, in order, to the tile's slice
 // of a staging area; the n-2 quirk (fill_comp_input :162-184) is one extra
-// staged slot: when x[n-2] == 0, a 0 precedes x[n-1]'s slot.
-template <int FT, bool kVec>
+// staged slot: when x[n-2] == 0, a 0 precedes x[n-1]'s slot.  (A persistent
+// grid streaming several tiles per workgroup measured slower: its live state
+// halves the occupancy, and a wave's wait for its next tile's loads also
+// drains its stores.)
+//
+// kHist: the staged words are also counted into the dense codec's symbol
+// histogram(s) (the compacted list's symbols, the n-2 slot included) and
+// added into row tile % nRows of [segments][nb][nRows][256] (PartialHist,
+// zeroed by the host), so the dense codec skips its histogram pass over the
+// list.
+template <int FT, bool kVec, bool kHist>
 __global__ __launch_bounds__(kThreads) void k_sparseCount(BatchDesc in, const uint64_t* outPtrs,
-                                                          uint32_t batchOffset, uint32_t tilesPerElem,
+                                                          uint32_t batchOffset, uint32_t numInBatch,
+                                                          uint32_t tilesPerElem,
                                                           uint32_t* __restrict__ tileCounts,
-                                                          WordOf<FT>* __restrict__ staging) {
+                                                          WordOf<FT>* __restrict__ staging,
+                                                          uint32_t* __restrict__ histRows, uint32_t nRows) {
   using W = WordOf<FT>;
+  constexpr int kSegs = FloatTraits<FT>::kSegs;
   constexpr uint32_t kSteps = kTileWords / kWaves / 64;
+  constexpr uint32_t kCols = 4;  // LDS counter columns per bin (lane & 3)
   __shared__ __attribute__((aligned(16))) W buf[kTileWords];
+  __shared__ __attribute__((aligned(16))) uint32_t hs[kHist ? kSegs : 1][kHist ? kNumSymbols * kCols : 4];
   __shared__ uint32_t waveCnt[kWaves];
   const uint32_t b = batchOffset + blockIdx.y;
   const uint32_t n = in.size(b);
@@ -104,6 +118,11 @@ __global__ __launch_bounds__(kThreads) void k_sparseCount(BatchDesc in, const ui
     if (tid == 0) tileCounts[uint64_t(b) * tilesPerElem + tile] = 0;
     return;
   }
+  if constexpr (kHist) {
+    for (int sg = 0; sg < kSegs; ++sg)
+      for (uint32_t i = tid; i < kNumSymbols * kCols / 4; i += kThreads)
+        *(lp<u32x4>)&hs[sg][4 * i] = u32x4{0, 0, 0, 0};
+  }
   gp<const W> x = (gp<const W>)in.start(b);
   // bitwise: -0.0 is "nonzero" (generate_bitmap :56); loaded with the tile
   const W xn2 = n >= 2 ? x[n - 2] : W(1);
@@ -111,15 +130,16 @@ __global__ __launch_bounds__(kThreads) void k_sparseCount(BatchDesc in, const ui
   __syncthreads();
   const uint32_t bmBytes = (n + 7) / 8, bmPad = roundUp(bmBytes, 16);
   const bool gap = xn2 == W(0);
-  uint64_t m[kSteps];
+  // (the step ballots are taken again in the compaction below: sixteen
+  // 64-bit masks held across the barrier cost registers, i.e. occupancy)
   uint32_t cnt = 0;
   uint64_t bmLane = 0;  // lane j < kSteps: the bitmap word of step j
 #pragma unroll
   for (uint32_t j = 0; j < kSteps; ++j) {
     const uint32_t q = w * (kTileWords / kWaves) + 64 * j;  // step's first word in the tile
-    m[j] = ballot(buf[q + lane] != W(0));
-    cnt += uint32_t(__popcll(m[j]));
-    bmLane = lane == j ? maskToBitmap(m[j]) : bmLane;
+    const uint64_t mj = ballot(buf[q + lane] != W(0));
+    cnt += uint32_t(__popcll(mj));
+    bmLane = lane == j ? maskToBitmap(mj) : bmLane;
     const uint32_t i0 = t0 + q;
     if (gap && i0 <= n - 1 && n - 1 < i0 + 64) cnt += 1;  // the extra slot
   }
@@ -144,14 +164,36 @@ __global__ __launch_bounds__(kThreads) void k_sparseCount(BatchDesc in, const ui
     const uint32_t q = w * (kTileWords / kWaves) + 64 * j;
     const uint32_t i = t0 + q + lane;
     const W v = buf[q + lane];
-    const uint32_t dst = pos + mbcnt(m[j]);
+    const uint64_t mj = ballot(v != W(0));
+    const uint32_t dst = pos + mbcnt(mj);
     if (i + 1 == n && gap) {
       st[dst] = W(0);
       if (v != W(0)) st[dst + 1] = v;
     } else if (v != W(0)) {
       st[dst] = v;
     }
-    pos += uint32_t(__popcll(m[j])) + ((gap && t0 + q <= n - 1 && n - 1 < t0 + q + 64) ? 1u : 0u);
+    if constexpr (kHist) {
+      auto count = [&](W y) {
+#pragma unroll
+        for (int sg = 0; sg < kSegs; ++sg)
+          atomicAdd(&hs[sg][compOf<FT>(y, sg) * kCols + (lane & (kCols - 1))], 1u);
+      };
+      if (i + 1 == n && gap) count(W(0));
+      if (v != W(0)) count(v);
+    }
+    pos += uint32_t(__popcll(mj)) + ((gap && t0 + q <= n - 1 && n - 1 < t0 + q + 64) ? 1u : 0u);
+  }
+  if constexpr (kHist) {
+    __syncthreads();
+    for (int sg = 0; sg < kSegs; ++sg) {
+      uint32_t sum = 0;
+#pragma unroll
+      for (uint32_t k = 0; k < kCols; ++k) sum += hs[sg][tid * kCols + ((k + tid) & (kCols - 1))];
+      // few adds per address: the tiles of an element spread over nRows rows
+      if (sum)
+        __hip_atomic_fetch_add(G(histRows) + ((uint64_t(sg) * numInBatch + b) * nRows + tile % nRows) * kNumSymbols + tid,
+                               sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
 }
 
@@ -356,15 +398,32 @@ void sparseCompressT(StackDeviceMemory& res, const FloatCompressConfig& config, 
   auto list = res.alloc<uint8_t>(s, size_t(nb) * listStride);
   BatchDesc lists = BatchDesc::strided(list.data(), listStride, 0);
   lists.sizes = listLen.data();
+  // the list's symbol histogram, counted here for a single element when the
+  // three-kernel dense path follows (the single-pass compressor counts as it
+  // loads).  It saves the dense path's histogram launches (c4 1 x 15M fp32:
+  // compress 85 -> 75 us) but lengthens every tile's workgroup, so with
+  // more elements the separate k_hist over the compacted lists is faster
+  // (5 x 15M: 155 us against 170).
+  const bool countHist = nb == 1 && (FT == 4 || !persistentFits(maxN));
+  constexpr int kSegs = FloatTraits<FT>::kSegs;
+  // histogram rows: up to 64 per element, accumulated with atomics
+  const uint32_t G = tiles;
+  const uint32_t R = std::min(tiles, kReduceRows);
+  auto hist = res.alloc<uint32_t>(s, countHist ? size_t(kSegs) * nb * R * kNumSymbols : 1);
+  if (countHist) HIP_CHECK(hipMemsetAsync(hist.data(), 0, size_t(kSegs) * nb * R * kNumSymbols * 4, s));
   for (uint32_t y0 = 0; y0 < nb; y0 += kMaxGridY) {
     const uint32_t ny = std::min(kMaxGridY, nb - y0);
     prof::Scope p("sparse", s);
+    auto launch = [&](auto vecTag, auto histTag) {
+      k_sparseCount<FT, decltype(vecTag)::value, decltype(histTag)::value><<<dim3(G, ny), kThreads, 0, s>>>(
+          in, outPtrs_dev, y0, nb, tiles, tileCounts.data(), staging.data(), hist.data(), R);
+    };
     if (inAligned16) {
-      k_sparseCount<FT, true><<<dim3(tiles, ny), kThreads, 0, s>>>(in, outPtrs_dev, y0, tiles, tileCounts.data(),
-                                                                    staging.data());
+      if (countHist) launch(std::true_type{}, std::true_type{});
+      else launch(std::true_type{}, std::false_type{});
     } else {
-      k_sparseCount<FT, false><<<dim3(tiles, ny), kThreads, 0, s>>>(in, outPtrs_dev, y0, tiles, tileCounts.data(),
-                                                                     staging.data());
+      if (countHist) launch(std::false_type{}, std::true_type{});
+      else launch(std::false_type{}, std::false_type{});
     }
     HIP_LAUNCH_CHECK();
     k_sparseScan<<<ny, kThreads, 0, s>>>(y0, tiles, nullptr, in, tileCounts.data(), listLen.data());
@@ -373,7 +432,9 @@ void sparseCompressT(StackDeviceMemory& res, const FloatCompressConfig& config, 
                                                              staging.data(), lists);
     HIP_LAUNCH_CHECK();
   }
-  floatCompressDescs(res, config, nb, lists, maxN, denseOut, outSize_dev, s, nullptr, true);
+  const PartialHist pre{hist.data(), R};
+  floatCompressDescs(res, config, nb, lists, maxN, denseOut, outSize_dev, s, nullptr, true,
+                     countHist ? &pre : nullptr);
   if (outSize_dev) {
     k_sparseAddSizes<<<divUp(nb, 128), 128, 0, s>>>(in, nb, outSize_dev);
     HIP_LAUNCH_CHECK();

@@ -36,7 +36,10 @@ constexpr uint32_t kEpochMask = 0xffffu;
 // its own, so a stale word only ever overlaps a stale word of the same kind
 // (a tag collision across kinds -- say a look-back flag's value bits read as
 // a partial's epoch -- cannot happen whatever the shapes of earlier calls).
-enum SyncRegion : int { kSyncCounters = 0, kSyncFlags, kSyncPartials, kSyncLog, kSyncRegions };
+// kSyncArrive holds the three-kernel path's last-arrival counters (NormArgs,
+// encode.h): untagged, they wrap back to zero at every element's last
+// arrival, so they are zero between calls.
+enum SyncRegion : int { kSyncCounters = 0, kSyncFlags, kSyncPartials, kSyncLog, kSyncArrive, kSyncRegions };
 
 class SyncLease {
  public:
