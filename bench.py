@@ -394,8 +394,10 @@ def _extras(dev, pb, reps=3):
         torch.cuda.empty_cache()
 
     # per-call latency of the torch ops (host validation + launch) on a small
-    # batch: 8 x 4096 bf16, the kernels themselves take a few microseconds
-    xs = [torch.randn(4096, device=dev).to(torch.bfloat16) for _ in range(8)]
+    # batch: 8 x 4096 fp16, the kernels themselves take a few microseconds
+    # (fp16, not bf16: these 220 small launches would otherwise share the
+    # headline kernels' names in a rocprofv3 --stats summary of this command)
+    xs = [torch.randn(4096, device=dev).to(torch.float16) for _ in range(8)]
     tmp = torch.empty([64 << 20], dtype=torch.uint8, device=dev)
     comp, csz, _ = torch.ops.dietgpu.compress_data(True, xs, False, tmp)
     rows = [comp[i, : int(csz[i])] for i in range(len(xs))]
@@ -413,7 +415,7 @@ def _extras(dev, pb, reps=3):
         torch.cuda.synchronize()
         t_all = (time.perf_counter() - t0) / 200
         lat[name] = {"host_us_per_call": round(t_host * 1e6, 2), "us_per_call_synced": round(t_all * 1e6, 2)}
-    out.append({"config": "torch.ops.dietgpu per-call latency, 8 x 4096 bf16, 64 MiB temp_mem", **lat})
+    out.append({"config": "torch.ops.dietgpu per-call latency, 8 x 4096 fp16, 64 MiB temp_mem", **lat})
     del xs, tmp, comp, rows, outs
 
     # c4: fp64 two-pass (16,777,216 words) and 90 %-sparse fp32 (15,000,000)
@@ -468,8 +470,11 @@ def _pmc_traffic(kernel, ft):
     def natural(f):  # r01_v10 after r01_v9
         return [int(t) if t.isdigit() else t for t in re.split(r"(\d+)", os.path.basename(f))]
 
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")), key=natural)
-    for f in reversed(files):  # newest summary first
+    # newest summary first; within a round the profile of the driver's own
+    # command (profiles/rNN_driver_cmd_pmc.json) before the others
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")),
+                   key=lambda f: (natural(f)[:2], "driver_cmd" in f, natural(f)))
+    for f in reversed(files):
         try:
             d = json.load(open(f))
         except Exception:
