@@ -107,6 +107,15 @@ DEQ_EARLY = DEQ_A + """
 R_POLL = [(P, POLL_PAR, POLL_SER)]
 R_DEQ = [(P, DEQ_A, DEQ_EARLY), (P, "      if (d != ~0u && lane == 0) {", "      if (d != ~0u && lane == 0 && d == 0x7fffffffu) {")]
 R_Z = [(P, "(A().epoch & 1u) + z, 1ull", "(A().epoch & 1u), 1ull")]
+# round-3 decode LDS attribution (outputs invalid; bench --no-verify only)
+DH = "decode.h"
+D_TBL = [(DH, "  for (int c = 0; c < NC; ++c) e[c] = lut[c][p[c]->x & mask];",
+          "  for (int c = 0; c < NC; ++c) e[c] = lut[c][(p[c]->x & 0u) + (threadIdx.x & 63u)];")]
+D_RING = [(DH, "    v[c] = q.ringLane[idx & (dec::kRing - 1)];", "    v[c] = q.ringLane[(idx & 0u) + (threadIdx.x & 31u)];")]
+D_SEG = [(DH, "              for (int s = 0; s < S; ++s) segLane[c][s][tr * 32] = uint16_t(e0[c * S + s] >> 16);",
+          "              for (int s = 0; s < S; ++s) if (e0[c * S + s] == 0x12345u) segLane[c][s][tr * 32] = uint16_t(e0[c * S + s] >> 16);")]
+ENC512 = [("encode.h", "  constexpr uint32_t R = kFused ? enc::kRingFused : enc::kRing;",
+           "  constexpr uint32_t R = kFused ? (FT == 0 ? enc::kRingFused : 512u) : enc::kRing;")]
 SP = "sparse.hip"
 VARS = {
     "encprio": [("encode.h", "    // every wave's slot stores are complete before other waves copy them\n    asm volatile(\"s_waitcnt vmcnt(0)\" ::: \"memory\");", "    __builtin_amdgcn_s_setprio(2);\n    // every wave's slot stores are complete before other waves copy them\n    asm volatile(\"s_waitcnt vmcnt(0)\" ::: \"memory\");")],
@@ -137,6 +146,10 @@ VARS = {
     "prhalfalt": PRIO3("((blockIdx.x / A().slotSpan) >> 1) ^ (round & 1u)"),
     "pr3rotrev": PRIO3("(3u - (blockIdx.x / A().slotSpan) + round) % 3u"),
     "stamp": STAMP,
+    "enc512": ENC512,
+    "d_tbl": D_TBL,
+    "d_ring": D_RING,
+    "d_seg": D_SEG,
     "r_poll": R_POLL,
     "r_deq": R_DEQ,
     "r_z": R_Z,
