@@ -7,9 +7,10 @@
 // MI355X design:
 //  * The step is a chain of two dependent LDS round trips (table entry, then
 //    the renormalisation word), so throughput comes from independent chains:
-//    256-thread workgroups (4 waves), and every wave runs K = 4 block pairs
-//    (fp64: 2 pairs x 2 streams) -- lanes 0-31 one block, lanes 32-63 the
-//    next (the reference's 32-state interleaving).  16 chains per SIMD.
+//    256-thread workgroups (4 waves), every wave one block pair (K = 1; fp64:
+//    the pair's 2 streams) -- lanes 0-31 one block, lanes 32-63 the next (the
+//    reference's 32-state interleaving) -- and many resident waves (more,
+//    smaller waves beat 2-4 interleaved pairs per wave, DecCfg below).
 //  * 64-bit decode table {pdf | sym << 24, slot - cdf}: the state update is
 //    one v_mad_u32_u24 (u24 ignores the symbol byte); `entry >> 16` =
 //    sym << 8 is stored with ds_write_b16_d16_hi, already the high byte of an
