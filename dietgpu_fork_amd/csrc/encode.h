@@ -162,48 +162,76 @@ __device__ __forceinline__ void normalizeWave(uint32_t (&c)[4], uint32_t (&cdf)[
 // Encode table entry (internal, never archived) of a symbol with pdf q and
 // cumulative frequency cdf:
 //   x = pdf << (31 - pb)              renormalisation threshold
-//   y = magic                         x / pdf == (umulhi(x, magic) + x) >> shift
-//   z = cdf
-//   w = (2^pb - pdf) | shift << 24    x' = x + cdf + (x / pdf) * (2^pb - pdf)
-// magic(q) = 2^32 * (2^shift - q) / q + 1 with shift = ceil(log2 q), for
-// every pdf 1 <= q <= 2^11, computed at compile time (a 64-bit division per
-// symbol is ~100 VALU instructions)
+//   y = magic m                       x / pdf == umulhi(x, m) >> shift
+//   z = cdf (+ 2^pb - 1 for pdf 1)
+//   w = (2^pb - pdf) | shift << 24    x' = x + z + (x / pdf) * (2^pb - pdf)
+// The dividend is the state after renormalisation, x < pdf << (31 - pb) <=
+// 2^31, so a 32-bit magic suffices (Granlund-Montgomery, N = 31): with
+// l = ceil(log2 q) >= 1, m = ceil(2^(31+l) / q) < 2^32 satisfies
+// 2^(31+l) <= m q <= 2^(31+l) + 2^l, hence floor(x / q) =
+// floor(x m / 2^(31+l)) = umulhi(x, m) >> (l - 1) for every x < 2^31: two
+// VALU operations, not the three of the 33-bit magic ((umulhi + x) >> l).
+// pdf 1 has no such magic; it takes m = 2^32 - 1, shift 0, i.e. the
+// quotient x - 1 (x >= 16 there: renormalised states of a pdf-1 symbol are
+// >= 2^15 or >= 2^(31-pb) >> 16), and the one missing (2^pb - 1) goes into
+// z: x' = x 2^pb + cdf as the reference computes (ans/GpuANSEncode.cuh:63-89).
+// Computed at compile time for every pdf 1 <= q <= 2^11 (a 64-bit division
+// per symbol is ~100 VALU instructions).
+__host__ __device__ constexpr uint32_t encMagic(uint32_t q, uint32_t* shift) {
+  if (q <= 1) {
+    *shift = 0;
+    return q ? 0xffffffffu : 0u;
+  }
+  uint32_t l = 0;
+  while ((1u << l) < q) ++l;
+  *shift = l - 1;
+  return uint32_t(((1ull << (31 + l)) + q - 1) / q);
+}
 struct MagicTable {
   uint32_t m[(1u << 11) + 1];
   constexpr MagicTable() : m() {
     for (uint32_t q = 1; q <= (1u << 11); ++q) {
       uint32_t sh = 0;
-      while ((1u << sh) < q) ++sh;
-      m[q] = uint32_t(((1ull << 32) * ((1ull << sh) - q)) / q + 1);
+      m[q] = encMagic(q, &sh);
     }
   }
 };
 __device__ constexpr MagicTable kMagic{};
 
+__device__ __forceinline__ uint4 encEntryPack(uint32_t q, uint32_t cdf, uint32_t magic, uint32_t shift,
+                                              int pb) {
+  const uint32_t z = cdf + (q == 1 ? (1u << pb) - 1 : 0u);
+  return make_uint4(q << (kStateBits - pb), magic, z, ((1u << pb) - q) | (shift << 24));
+}
+
 __device__ __forceinline__ uint4 encTableEntry(uint32_t q, uint32_t cdf, int pb) {
   uint32_t shift = 0, magic = 0;
-  if (q > 0) {
-    shift = 32 - __clz(q - 1);
+  if (q > 1) {
+    shift = 31 - __clz(q - 1);  // ceil(log2 q) - 1
     magic = kMagic.m[q];
+  } else if (q == 1) {
+    magic = 0xffffffffu;
   }
-  return make_uint4(q << (kStateBits - pb), magic, cdf, ((1u << pb) - q) | (shift << 24));
+  return encEntryPack(q, cdf, magic, shift, pb);
 }
 
 // The same entry with the magic computed in registers (no dependent global
-// load of kMagic on a latency-bound path): floor((2^shift - q) 2^32 / q) + 1
-// from a double division (the numerator < 2^43 is exact; the quotient is
-// within one of the floor) and an exact integer fix-up.
+// load of kMagic on a latency-bound path): ceil(2^(31+l) / q) from a double
+// division (the numerator 2^(31+l) <= 2^42 is exact; the quotient is within
+// one of the floor) and an exact integer fix-up.
 __device__ __forceinline__ uint4 encTableEntryReg(uint32_t q, uint32_t cdf, int pb) {
   uint32_t shift = 0, magic = 0;
-  if (q > 0) {
-    shift = 32 - __clz(q - 1);
-    const uint64_t num = ((1ull << shift) - q) << 32;
-    uint64_t m = uint64_t(double(num) / double(q));
+  if (q > 1) {
+    shift = 31 - __clz(q - 1);
+    const uint64_t num = 1ull << (32 + shift);
+    uint64_t m = uint64_t(double(num) / double(q));  // ~floor(num / q)
     if (m * q > num) m -= 1;
     else if ((m + 1) * q <= num) m += 1;
-    magic = uint32_t(m + 1);
+    magic = uint32_t(m + (m * q != num));  // ceil
+  } else if (q == 1) {
+    magic = 0xffffffffu;
   }
-  return make_uint4(q << (kStateBits - pb), magic, cdf, ((1u << pb) - q) | (shift << 24));
+  return encEntryPack(q, cdf, magic, shift, pb);
 }
 
 // ---------------------------------------------------------------------------
@@ -622,8 +650,7 @@ __device__ __forceinline__ void encStep(EStream& p, bool valid, const u32x4& e, 
   asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(dst) : "v"(trashAddr), "v"(ringAddr), "s"(vote));
   *(lp<uint16_t>)size_t(dst) = uint16_t(p.x);
   (void)wr;
-  uint32_t q = __umulhi(x, e.y);
-  q = (q + x) >> (e.w >> 24);
+  const uint32_t q = __umulhi(x, e.y) >> (e.w >> 24);
   const uint32_t xn = __umul24(q, e.w) + x + e.z;  // u24 ignores the shift byte
   p.x = (!kMask || valid) ? xn : x;
 }

@@ -117,7 +117,16 @@ D_SEG = [(DH, "              for (int s = 0; s < S; ++s) segLane[c][s][tr * 32] 
 ENC512 = [("encode.h", "  constexpr uint32_t R = kFused ? enc::kRingFused : enc::kRing;",
            "  constexpr uint32_t R = kFused ? (FT == 0 ? enc::kRingFused : 512u) : enc::kRing;")]
 SP = "sparse.hip"
+# round 3: writers' ring store under an exec mask (2 SALU) instead of the
+# trash-address select (1 VALU)
+XW = [("encode.h", """  uint32_t dst;
+  asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(dst) : "v"(trashAddr), "v"(ringAddr), "s"(vote));
+  *(lp<uint16_t>)size_t(dst) = uint16_t(p.x);""", r"""  uint64_t sav_;
+  (void)trashAddr;
+  asm volatile("s_and_saveexec_b64 %0, %1\n\tds_write_b16 %2, %3\n\ts_mov_b64 exec, %0"
+               : "=&s"(sav_) : "s"(vote), "v"(ringAddr), "v"(p.x) : "memory", "scc");""")]
 VARS = {
+    "xw": XW,
     "encprio": [("encode.h", "    // every wave's slot stores are complete before other waves copy them\n    asm volatile(\"s_waitcnt vmcnt(0)\" ::: \"memory\");", "    __builtin_amdgcn_s_setprio(2);\n    // every wave's slot stores are complete before other waves copy them\n    asm volatile(\"s_waitcnt vmcnt(0)\" ::: \"memory\");")],
     "d3": [(P, "  constexpr int D = 2;", "  constexpr int D = 3;")],
     "sp_nolb": [(SP, "    const uint32_t excl =\n        lookBackPoison(G(flags) + uint64_t(b) * tilesPerElem, tile, total, epoch, spinCap, pz);", "    const uint32_t excl = tile * 409u; (void)total;")],
