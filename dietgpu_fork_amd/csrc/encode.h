@@ -25,74 +25,10 @@ constexpr int kWaves = kThreads / 64;
 constexpr uint32_t kSlotBytes = kStateBytesPerBlock + kSlotDataBytes;
 
 // Bit-exact restatement of normalizeProbabilitiesFromHistogram
-// (ans/GpuANSStatistics.cuh:178-366) for one kThreads-thread workgroup, thread
-// s = symbol s: float32 quantisation, descending order of the unique keys
-// (q << 16) | sym by rank counting (in place of cub::BlockRadixSort), the
-// diff > 0 bump of *symbol ids* < diff, and the diff < 0 decrement of sorted
-// ranks [g-k, g).  Returns this symbol's pdf.  total > 0; whole workgroup.
-__device__ __forceinline__ uint32_t normalizeCount(uint32_t count, uint32_t total, int pb,
-                                                   uint32_t* keys, uint32_t* red) {
-  const uint32_t s = threadIdx.x;
-  const uint32_t W = 1u << pb;
-  const float r = __fdiv_rn(float(count), float(total));
-  const float f = __fmul_rn(float(W), r);
-  uint32_t q = uint32_t(f);
-  if (count > 0 && q == 0) q = 1;
-  const uint32_t qsum = blockSum<kThreads>(q, red);
-
-  const int diff = int(W) - int(qsum);
-  if (diff > 0) {
-    q += uint32_t(diff) / kNumSymbols + (s < uint32_t(diff) % kNumSymbols ? 1u : 0u);
-  } else if (diff < 0) {
-    // Only entries with q > 1 are ever decremented, and they form a prefix
-    // [0, g) of the descending key order, so a symbol's rank among the
-    // (typically ~20) keys with q > 1 equals its rank in the full sort.
-    const uint32_t key = (q << 16) | s;
-    uint32_t g0;
-    const uint32_t pos = blockExclusiveScan<kThreads>(q > 1 ? 1u : 0u, red, &g0);
-    if (q > 1) keys[pos] = key;
-    __syncthreads();
-    uint32_t rank = kNumSymbols;
-    if (q > 1) {
-      rank = 0;
-      for (uint32_t t = 0; t < g0; ++t) rank += keys[t] > key ? 1u : 0u;
-    }
-    __syncthreads();
-    if (q > 1) keys[rank] = q;  // the q > 1 values in rank order
-    __syncthreads();
-    if (threadIdx.x < 64) {
-      // the reference's rounds, on one wave: each takes 1 from the k = min(d,
-      // g) lowest-ranked of the g entries still > 1
-      const uint32_t lane = threadIdx.x;
-      uint32_t Q[kNumSymbols / 64];
-#pragma unroll
-      for (uint32_t j = 0; j < kNumSymbols / 64; ++j) Q[j] = lane + 64 * j < g0 ? keys[lane + 64 * j] : 1u;
-      int d = -diff;
-      while (d > 0) {
-        int g = 0;
-#pragma unroll
-        for (uint32_t j = 0; j < kNumSymbols / 64; ++j) g += __popcll(ballot(Q[j] > 1));
-        if (g == 0) break;  // reference asserts; unreachable for real tables
-        const int k = d < g ? d : g;
-#pragma unroll
-        for (uint32_t j = 0; j < kNumSymbols / 64; ++j) {
-          const int r = int(lane + 64 * j);
-          if (r >= g - k && r < g) Q[j] -= 1;
-        }
-        d -= k;
-      }
-#pragma unroll
-      for (uint32_t j = 0; j < kNumSymbols / 64; ++j)
-        if (lane + 64 * j < g0) keys[lane + 64 * j] = Q[j];
-    }
-    __syncthreads();
-    if (q > 1) q = keys[rank];
-  }
-  return q;
-}
-
-// The same normalisation by ONE wave, lane l holding symbols 4l + j
-// (j < 4), in registers only: no workgroup barrier (the other waves of a
+// (ans/GpuANSStatistics.cuh:178-366) -- float32 quantisation, the diff > 0
+// bump of symbol ids < diff, the diff < 0 decrement rounds over the
+// descending (q << 16) | sym order -- by ONE wave, lane l holding symbols
+// 4l + j (j < 4), in registers only: no workgroup barrier (the other waves of a
 // workgroup work meanwhile) and no LDS round trip (queued behind the other
 // workgroups' traffic, a dozen of them took microseconds).  c[j]: the
 // counts in, the pdfs out; cdf[j]: the exclusive cumulative pdfs (symbol
@@ -236,7 +172,7 @@ __device__ __forceinline__ uint4 encTableEntryReg(uint32_t q, uint32_t cdf, int 
 
 // ---------------------------------------------------------------------------
 // Normalisation of one (element, segment): sums the partial histograms,
-// normalises (normalizeCount) and stores the encode table rows
+// normalises (normalizeWave) and stores the encode table rows
 // (encTableEntry) and the u16 pdf.  Run by k_normalize, or -- one launch
 // fewer -- by the last workgroup to finish an element in the kernel that
 // writes its final partial rows (k_hist or k_histReduce: NormArgs::arrive,
@@ -323,10 +259,26 @@ __device__ __forceinline__ void normalizeElement(const NormArgs& a, uint32_t num
     G(a.pdf)[row * kNumSymbols + s] = 0;
     return;
   }
-  const uint32_t q = normalizeCount(count, total, a.pb, keys, red);
-  const uint32_t cdf = blockExclusiveScan<kThreads>(q, red, nullptr);
-  st16(G(a.table) + row * kNumSymbols + s, encTableEntry(q, cdf, a.pb));
-  G(a.pdf)[row * kNumSymbols + s] = uint16_t(q);
+  // one wave normalises in registers (normalizeWave: no workgroup barriers,
+  // no LDS rank sort) and computes the table entries' magics in registers
+  // (no dependent load of kMagic): on these latency-bound single-workgroup
+  // tails that is most of the kernel
+  keys[s] = count;
+  __syncthreads();
+  if (s < 64) {
+    uint32_t c[4], cdf[4];
+    const u32x4 kv = *(lp<const u32x4>)&keys[4 * s];
+    c[0] = kv.x;
+    c[1] = kv.y;
+    c[2] = kv.z;
+    c[3] = kv.w;
+    normalizeWave(c, cdf, total, a.pb);
+    gp<uint4> trow = G(a.table) + row * kNumSymbols + 4 * s;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) st16(trow + j, encTableEntryReg(c[j], cdf[j], a.pb));
+    st8((gp<uint8_t>)(G(a.pdf) + row * kNumSymbols + 4 * s), make_uint2(c[0] | (c[1] << 16), c[2] | (c[3] << 16)));
+  }
+  __syncthreads();  // keys reusable
 }
 
 // After this workgroup's rows of element b are stored -- with sc1 stores --
@@ -347,7 +299,7 @@ __device__ __forceinline__ bool lastArrival(uint32_t* counter, uint32_t arrivals
 
 static __global__ __launch_bounds__(kThreads) void k_normalize(NormArgs a, uint32_t batchOffset,
                                                                uint32_t numInBatch) {
-  __shared__ uint32_t keys[kNumSymbols];
+  __shared__ __attribute__((aligned(16))) uint32_t keys[kNumSymbols];
   __shared__ uint32_t red[kWaves];
   __shared__ u32x4 red4[kThreads];
   normalizeElement(a, numInBatch, batchOffset + blockIdx.x, blockIdx.y, keys, red, red4);
@@ -496,7 +448,7 @@ static __global__ __launch_bounds__(kThreads) void k_histReduce(
     uint32_t batchOffset, uint32_t numInBatch, uint32_t chunksPerElem, uint32_t groups,
     const uint32_t* __restrict__ part, const uint32_t* __restrict__ partCk,
     uint32_t* __restrict__ outHist, uint32_t* __restrict__ outCk, NormArgs na, uint32_t segs) {
-  __shared__ uint32_t keys[kNumSymbols];
+  __shared__ __attribute__((aligned(16))) uint32_t keys[kNumSymbols];
   __shared__ uint32_t red[kWaves + 1];
   __shared__ u32x4 red4[kThreads];
   const uint32_t b = batchOffset + blockIdx.y;
@@ -531,7 +483,7 @@ static __global__ __launch_bounds__(kThreads) void k_histReduce(
 //     section, ANS symbols to LDS.  It then runs 16 branch-free encode steps
 //     per block from LDS (fully unrolled).
 //   * Emitted u16 words go to an LDS ring per block stream (writers at
-//     ascending lane order; non-writers store to a per-lane trash dword so
+//     ascending lane order, stored under an exec mask so
 //     the step has no branch).  fp64 (512-word rings): flushed to the block's
 //     scratch slot 256 words at a time with one 8 B store per lane, and
 //     k_coalesce packs the slots into the archive.  Single-segment formats
@@ -613,8 +565,7 @@ __device__ __forceinline__ void ringFlushAll(EStream& p, uint32_t lane) {
 // ascending lane order.  hv: all-ones on lanes 32-63 (opaque to the
 // compiler).  Masked (!valid) lanes neither write nor change state.
 template <bool kMask, uint32_t kRing = enc::kRing>
-__device__ __forceinline__ void encStep(EStream& p, bool valid, const u32x4& e, uint32_t hv,
-                                        uint32_t trashAddr) {
+__device__ __forceinline__ void encStep(EStream& p, bool valid, const u32x4& e, uint32_t hv) {
   bool wr = true;
   uint64_t vote;
   uint32_t x;  // the state after renormalisation
@@ -644,11 +595,16 @@ __device__ __forceinline__ void encStep(EStream& p, bool valid, const u32x4& e, 
   const uint32_t idx = __builtin_amdgcn_mbcnt_hi(uint32_t(vote >> 32),
                                                  __builtin_amdgcn_mbcnt_lo(uint32_t(vote), vbase));
   const uint32_t ringAddr = uint32_t(size_t(p.ringLane + (idx & (kRing - 1))));
-  // non-writers store to their trash dword: one v_cndmask on the ballot mask
-  // and an unconditional ds_write, no exec-mask split of the step
-  uint32_t dst;
-  asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(dst) : "v"(trashAddr), "v"(ringAddr), "s"(vote));
-  *(lp<uint16_t>)size_t(dst) = uint16_t(p.x);
+  // writers store under an exec mask set in the asm itself: two SALU
+  // instructions, no VALU select and no split of the step's control flow
+  // (the LDS ops of a wave complete in order,
+  // so the compiler's later lgkmcnt waits stay conservative; "memory" keeps
+  // the ring reads of the flushes after it)
+  uint64_t sav;
+  asm volatile("s_and_saveexec_b64 %0, %1\n\tds_write_b16 %2, %3\n\ts_mov_b64 exec, %0"
+               : "=&s"(sav)
+               : "s"(vote), "v"(ringAddr), "v"(p.x)
+               : "memory", "scc");
   (void)wr;
   const uint32_t q = __umulhi(x, e.y) >> (e.w >> 24);
   const uint32_t xn = __umul24(q, e.w) + x + e.z;  // u24 ignores the shift byte
@@ -944,7 +900,6 @@ __global__ __launch_bounds__(enc::kThreads) void k_encode(BatchDesc in, BatchDes
   __shared__ __attribute__((aligned(16))) uint32_t tblS[S][kNumSymbols * 4];
   __shared__ __attribute__((aligned(16))) uint8_t symS[Cfg::kHalfStreams][enc::kSegWords];
   __shared__ __attribute__((aligned(16))) uint16_t ringS[Cfg::kHalfStreams / 2][2 * R];
-  __shared__ uint32_t trashS[enc::kWaves][64];
   __shared__ uint32_t cwE[Cfg::kBlocksPerWG];
   __shared__ uint32_t flE[Cfg::kBlocksPerWG];
   __shared__ uint32_t preE[Cfg::kBlocksPerWG];
@@ -976,7 +931,6 @@ __global__ __launch_bounds__(enc::kThreads) void k_encode(BatchDesc in, BatchDes
   gp<const WordT> src = (gp<const WordT>)startOf(in, b);
   gp<uint8_t> raw = FT == 0 ? gp<uint8_t>(nullptr) : startOf(out, b) + 32;
   const bool vecIn = (reinterpret_cast<uintptr_t>(src) & 15) == 0;
-  const uint32_t trashAddr = uint32_t(size_t((lp<uint32_t>)&trashS[w][lane]));
 
   uint32_t uwH[K][2];  // wave-uniform
   uint32_t blk[K], uw[K];
@@ -1095,7 +1049,7 @@ __global__ __launch_bounds__(enc::kThreads) void k_encode(BatchDesc in, BatchDes
 #pragma unroll
           for (int c = 0; c < K; ++c)
 #pragma unroll
-            for (int s = 0; s < S; ++s) encStep<false, R>(st[c][s], true, E[u][c][s], hv, trashAddr);
+            for (int s = 0; s < S; ++s) encStep<false, R>(st[c][s], true, E[u][c][s], hv);
       }
       __builtin_amdgcn_wave_barrier();
     }
@@ -1122,7 +1076,7 @@ __global__ __launch_bounds__(enc::kThreads) void k_encode(BatchDesc in, BatchDes
           for (int s = 0; s < S; ++s) {
             const uint32_t sym = valid ? uint32_t(symLane[c][s][tr * 32]) : 0u;
             const u32x4 e = tbl[s][sym];
-            encStep<true, R>(st[c][s], valid, e, hv, trashAddr);
+            encStep<true, R>(st[c][s], valid, e, hv);
           }
         }
       }

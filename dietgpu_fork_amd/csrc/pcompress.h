@@ -213,7 +213,6 @@ __global__ __launch_bounds__(pc::kThreads) __attribute__((amdgpu_waves_per_eu(4,
   __shared__ __attribute__((aligned(16))) uint16_t rings[pc::kBlocksPerItem * pc::kRing];
   __shared__ __attribute__((aligned(16))) uint32_t tblS[kNumSymbols * 4];
   __shared__ __attribute__((aligned(16))) uint8_t symT[pc::kBlocksPerItem][pc::kSegWords];
-  __shared__ __attribute__((aligned(16))) uint32_t trashS[pc::kWaves][64];
   __shared__ __attribute__((aligned(16))) uint16_t pdfS[kNumSymbols];
   __shared__ uint32_t ckS[pc::kWaves];
   __shared__ __attribute__((aligned(16))) uint32_t cwE[pc::kBlocksPerItem];
@@ -244,7 +243,6 @@ __global__ __launch_bounds__(pc::kThreads) __attribute__((amdgpu_waves_per_eu(4,
   auto tidNow = [&]() __attribute__((always_inline)) -> uint32_t { return (w << 6) + laneNow(); };
   uint32_t hv = halfNow() ? ~0u : 0u;
   asm volatile("" : "+v"(hv));  // keep `hv & x` a v_and
-  const uint32_t trashAddr = uint32_t(size_t((lp<uint32_t>)&trashS[w][lane]));
   lp<uint32_t> hcol = (lp<uint32_t>)&hist[l & (pc::kHistCols - 1)];
   // quad byte transpose of the symbols (phase 1): lane l = 4 qm + qr
   const uint32_t qr = l & 3, qm = l >> 2;
@@ -466,7 +464,7 @@ __global__ __launch_bounds__(pc::kThreads) __attribute__((amdgpu_waves_per_eu(4,
         Ev[u] = tbl[(symR[t / 4] >> (8 * (t & 3))) & 0xffu];
       }
 #pragma unroll
-      for (uint32_t u = 0; u < enc::kUnroll; ++u) encStep<false, pc::kRing>(p, true, Ev[u], hv, trashAddr);
+      for (uint32_t u = 0; u < enc::kUnroll; ++u) encStep<false, pc::kRing>(p, true, Ev[u], hv);
       // keep the scheduler from hoisting later groups' table reads over the
       // ring stores (registers, not latency, bound this loop)
       __builtin_amdgcn_sched_barrier(0);
@@ -485,7 +483,7 @@ __global__ __launch_bounds__(pc::kThreads) __attribute__((amdgpu_waves_per_eu(4,
 #pragma unroll
       for (uint32_t u = 0; u < enc::kUnroll; ++u) {
         const uint32_t t = t0 + u;
-        encStep<true, pc::kRing>(p, t * 32 + l < uw, Ev[u], hv, trashAddr);
+        encStep<true, pc::kRing>(p, t * 32 + l < uw, Ev[u], hv);
       }
       __builtin_amdgcn_sched_barrier(0);
     }
