@@ -202,7 +202,8 @@ bool persistentFits(uint32_t maxWords) {
 template <int FT, bool kCk>
 bool compressPersistent(StackDeviceMemory& res, int pb, bool useChecksum, uint32_t nb,
                         const BatchDesc& in, uint32_t maxSize, const BatchDesc& out,
-                        uint32_t* outSize_dev, hipStream_t s, const DeviceTables* tabs) {
+                        uint32_t* outSize_dev, hipStream_t s, const DeviceTables* tabs,
+                        const uint32_t* sparseN) {
   const uint32_t MB = divUp(maxSize, kBlockSize);
   const uint32_t team = std::max(1u, divUp(MB, pc::kBlocksPerItem));
   if (team > pc::kMaxTeam) return false;
@@ -262,6 +263,7 @@ bool compressPersistent(StackDeviceMemory& res, int pb, bool useChecksum, uint32
   a.teamStart = nullptr;
   a.ckIn = FT != 0 && useChecksum ? ck.data() : nullptr;
   a.outSize = outSize_dev;
+  a.sparseN = sparseN;
   a.items = items;
   a.team = team;
   a.nb = nb;
@@ -284,7 +286,8 @@ template <int FT>
 void encodeBatchDevice(StackDeviceMemory& res, int pb, bool useChecksum, uint32_t nb,
                        const BatchDesc& inArg, uint32_t maxSize, const uint32_t* hist_dev,
                        const BatchDesc& outArg, uint32_t* outSize_dev, hipStream_t s,
-                       const DeviceTables* tabs, bool inAligned16, const PartialHist* pre = nullptr) {
+                       const DeviceTables* tabs, bool inAligned16, const PartialHist* pre = nullptr,
+                       const uint32_t* sparseN = nullptr) {
   checkProbBits(pb);
   if (nb == 0) return;
   constexpr int kSegs = FloatTraits<FT>::kSegs;
@@ -299,9 +302,9 @@ void encodeBatchDevice(StackDeviceMemory& res, int pb, bool useChecksum, uint32_
   if constexpr (kFused) {
     if (!userHist && inAligned16) {
       const bool done = rawCk ? compressPersistent<FT, FT == 0>(res, pb, useChecksum, nb, inArg,
-                                                                 maxSize, outArg, outSize_dev, s, tabs)
+                                                                 maxSize, outArg, outSize_dev, s, tabs, sparseN)
                               : compressPersistent<FT, false>(res, pb, useChecksum, nb, inArg, maxSize,
-                                                              outArg, outSize_dev, s, tabs);
+                                                              outArg, outSize_dev, s, tabs, sparseN);
       if (done) return;
     }
   }
@@ -394,7 +397,7 @@ void encodeBatchDevice(StackDeviceMemory& res, int pb, bool useChecksum, uint32_
       prof::Scope p("encode", s);
       dim3 g(nW, ny);
       const EncTail tail{pdf.data(), ck.data(), outSize_dev, flags.data(), nW, pb, useChecksum,
-                         spinCap(), deviceErrorWord()};
+                         spinCap(), deviceErrorWord(), sparseN};
       k_encode<FT, 0><<<g, enc::kThreads, 0, s>>>(in, out, y0, nb, std::max(MB, 1u), table.data(),
                                                slots.data(), cw.data(), tail);
       HIP_LAUNCH_CHECK();
@@ -405,7 +408,7 @@ void encodeBatchDevice(StackDeviceMemory& res, int pb, bool useChecksum, uint32_
       dim3 g(std::max(1u, divUp(MB, bpw)), ny, kSegs);
       k_coalesce<FT><<<g, kThreads, 0, s>>>(in, out, y0, nb, std::max(MB, 1u), bpw, slots.data(),
                                             cw.data(), pdf.data(), pb, useChecksum, ck.data(),
-                                            outSize_dev);
+                                            outSize_dev, sparseN);
       HIP_LAUNCH_CHECK();
     }
   }
@@ -704,25 +707,25 @@ static void checkFloatConfig(const FloatCodecConfig& c) {
 void floatCompressDescs(StackDeviceMemory& res, const FloatCompressConfig& config, uint32_t nb,
                         const BatchDesc& in, uint32_t maxSize, const BatchDesc& out,
                         uint32_t* outSize_dev, hipStream_t s, const DeviceTables* tabs,
-                        bool inAligned16, const PartialHist* pre) {
+                        bool inAligned16, const PartialHist* pre, const uint32_t* sparseN) {
   checkFloatConfig(config);
   const int pb = config.ansConfig.probBits;
   switch (config.floatType) {
     case FloatType::kFloat16:
       encodeBatchDevice<1>(res, pb, config.useChecksum, nb, in, maxSize, nullptr, out, outSize_dev, s,
-                             tabs, inAligned16, pre);
+                             tabs, inAligned16, pre, sparseN);
       break;
     case FloatType::kBFloat16:
       encodeBatchDevice<2>(res, pb, config.useChecksum, nb, in, maxSize, nullptr, out, outSize_dev, s,
-                             tabs, inAligned16, pre);
+                             tabs, inAligned16, pre, sparseN);
       break;
     case FloatType::kFloat32:
       encodeBatchDevice<3>(res, pb, config.useChecksum, nb, in, maxSize, nullptr, out, outSize_dev, s,
-                             tabs, inAligned16, pre);
+                             tabs, inAligned16, pre, sparseN);
       break;
     default:
       encodeBatchDevice<4>(res, pb, config.useChecksum, nb, in, maxSize, nullptr, out, outSize_dev, s,
-                             tabs, inAligned16, pre);
+                             tabs, inAligned16, pre, sparseN);
       break;
   }
 }

@@ -24,7 +24,8 @@ struct PartialHist {
 void floatCompressDescs(StackDeviceMemory& res, const FloatCompressConfig& config, uint32_t nb,
                         const BatchDesc& in, uint32_t maxSize, const BatchDesc& out,
                         uint32_t* outSize_dev, hipStream_t s, const DeviceTables* tabs = nullptr,
-                        bool inAligned16 = false, const PartialHist* pre = nullptr);
+                        bool inAligned16 = false, const PartialHist* pre = nullptr,
+                        const uint32_t* sparseN = nullptr);
 
 // The single-pass compressor (k_pcompress) takes float elements of at most
 // this many words (and 16 B-aligned inputs).

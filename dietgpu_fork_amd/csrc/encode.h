@@ -769,7 +769,16 @@ struct EncTail {
   bool useChecksum;
   uint32_t spinCap = 1u << 24;  // look-back polls before the element is poisoned
   uint32_t* err = nullptr;      // device error word (poisoned elements)
+  // sparse archives: element sizes whose header + bitmap precede this dense
+  // archive (sparseOverhead), added to outSize; null otherwise
+  const uint32_t* sparseN = nullptr;
 };
+
+// bytes of a sparse archive before its dense part: 16 B header, bitmap
+// padded to 16 (float/GpuSparseFloatCompress.cuh)
+__device__ __forceinline__ uint64_t sparseOverhead(const uint32_t* sparseN, uint32_t b) {
+  return sparseN ? 16ull + roundUp64((uint64_t(sparseN[b]) + 7) / 8, 16) : 0ull;
+}
 
 constexpr uint64_t kFlagAgg = 1ull << 62;
 constexpr uint64_t kFlagPrefix = 2ull << 62;
@@ -877,6 +886,7 @@ __device__ __forceinline__ void writeHeadTotal(gp<uint8_t> base, gp<uint8_t> o, 
     ((gp<uint32_t>)base)[4] = uint32_t(roundUp64(ansBytes, 16));  // GpuFloatHeader2
     sz += 32ull + floatRawBytes(FT, n);
   }
+  sz += sparseOverhead(t.sparseN, b);
   if (t.outSize) G(t.outSize)[b] = uint32_t(sz);
 }
 
@@ -1163,7 +1173,7 @@ __global__ __launch_bounds__(kThreads) void k_coalesce(
     BatchDesc in, BatchDesc out, uint32_t batchOffset, uint32_t numInBatch, uint32_t MB,
     uint32_t blocksPerWG, const uint8_t* __restrict__ slots, const uint32_t* __restrict__ cw,
     const uint16_t* __restrict__ pdf, int pb, bool useChecksum,
-    const uint32_t* __restrict__ ck, uint32_t* __restrict__ outSize) {
+    const uint32_t* __restrict__ ck, uint32_t* __restrict__ outSize, const uint32_t* __restrict__ sparseN) {
   constexpr int kSegs = FloatTraits<FT>::kSegs;
   __shared__ uint32_t red[kWaves];
   __shared__ uint32_t pre[kThreads];
@@ -1231,6 +1241,7 @@ __global__ __launch_bounds__(kThreads) void k_coalesce(
         fh[7] = 0;
         uint64_t sz = 32ull + floatRawBytes(FT, n) + ansBytes;
         if (kSegs == 2) sz += ansOverhead(nBlocks) + 2ull * total1Words;
+        sz += sparseOverhead(sparseN, b);
         if (outSize) G(outSize)[b] = uint32_t(sz);
       }
     }

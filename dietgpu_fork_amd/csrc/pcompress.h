@@ -100,6 +100,7 @@ struct PCompArgs {
   const uint32_t* teamStart;  // [nb + 1] first item of each element, or null: uniform teams
   const uint32_t* ckIn;  // float checksum per element (k_checksum) or null
   uint32_t* outSize;
+  const uint32_t* sparseN;  // EncTail::sparseN
   uint32_t items;        // total items
   uint32_t team;         // items per element when uniform
   uint32_t nb;
@@ -590,7 +591,8 @@ __global__ __launch_bounds__(pc::kThreads) __attribute__((amdgpu_waves_per_eu(4,
           if (A().outSize) G(A().outSize)[it.b] = 0u;
           __hip_atomic_fetch_add(G(A().err), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         } else {
-          const EncTail t{nullptr, nullptr, A().outSize, nullptr, 0, A().pb, A().useChecksum};
+          EncTail t{nullptr, nullptr, A().outSize, nullptr, 0, A().pb, A().useChecksum};
+          t.sparseN = A().sparseN;
           writeHeadTotal<FT>(base, o, it.n, it.nBlocks, excl + agg, bwords, t, it.b);
         }
       }

@@ -8,9 +8,10 @@
 // here both directions are reduce-then-scan over 4096-word tiles, fully
 // stream-ordered (no host or device-wide sync): compression reads the input
 // ONCE (k_sparseCount: bitmap, tile counts, nonzeros compacted within the
-// tile into a staging area; k_sparseScan: tile offsets; k_sparseGather: the
-// staged nonzeros to their list positions), decompression scans the bitmap's
-// tile popcounts and expands.  (A decoupled look-back across the tiles of
+// tile into a staging area; k_sparseGather: each tile sums its element's
+// earlier tile counts and moves its staged nonzeros to their list
+// positions), decompression takes the bitmap's tile popcounts
+// (k_sparseHeaders) and expands (k_sparseExpand, the same per-tile prefix).  (A decoupled look-back across the tiles of
 // one element measured slower: with thousands of tiles its chain dominates.)
 //
 // Wire format: 16 B header {u32 N, 12 B zero}, bitmap
@@ -197,87 +198,51 @@ __global__ __launch_bounds__(kThreads) void k_sparseCount(BatchDesc in, const ui
   }
 }
 
-// s2 / d2: exclusive scan of tile counts per element (in place); optional
-// total (the compacted list's length).  grid (batch).  Thread t owns a
-// contiguous run of `per` tiles: one round of loads, one block scan, one
-// round of stores (a 256-wide loop over the tiles paid one memory latency per
-// 256 tiles: 8.8 us for c4's 3,662 tiles).
-__global__ __launch_bounds__(kThreads) void k_sparseScan(uint32_t batchOffset, uint32_t tilesPerElem,
-                                                         const uint32_t* __restrict__ sizes, BatchDesc in,
-                                                         uint32_t* __restrict__ tileCounts,
-                                                         uint32_t* __restrict__ total) {
-  constexpr uint32_t kR = 16;  // tiles per thread held in registers
-  __shared__ uint32_t red[kWaves];
-  const uint32_t b = batchOffset + blockIdx.x;
-  const uint32_t n = sizes ? sizes[b] : in.size(b);
-  const uint32_t tiles = min(divUp(n, kTileWords), tilesPerElem);
-  uint32_t* tc = tileCounts + uint64_t(b) * tilesPerElem;
-  const uint32_t per = divUp(tiles, kThreads);
-  const uint32_t t0 = threadIdx.x * per;
-  const uint32_t mine = t0 < tiles ? min(per, tiles - t0) : 0u;
-  uint32_t v[kR];
+// Sum of counts[0, k) by the whole workgroup: 16 loads in flight per thread
+// (4,096 counts per memory round trip; an element of 16 M words has 4,096
+// tiles).  Every workgroup of an element sums its own prefix of the tile
+// counts, which stay in L2 (a 15 M-word element: 14.6 KB of counts, 27 MB of
+// L2 reads over its 3,662 workgroups), instead of a separate scan launch
+// (each launch of this chain costs ~5 us, however little it does).
+__device__ __forceinline__ uint32_t tilePrefix(gp<const uint32_t> counts, uint32_t k, uint32_t* red) {
+  constexpr uint32_t kR = 16;
   uint32_t sum = 0;
-  if (per <= kR) {
-#pragma unroll
-    for (uint32_t j = 0; j < kR; ++j) v[j] = j < mine ? tc[t0 + j] : 0u;
-#pragma unroll
-    for (uint32_t j = 0; j < kR; ++j) sum += v[j];
-  } else {  // (elements over 16 M words) chunks of kR loads in flight
-    for (uint32_t k = 0; k < mine; k += kR) {
-#pragma unroll
-      for (uint32_t j = 0; j < kR; ++j) v[j] = k + j < mine ? tc[t0 + k + j] : 0u;
-#pragma unroll
-      for (uint32_t j = 0; j < kR; ++j) sum += v[j];
-    }
-  }
-  uint32_t all = 0;
-  uint32_t run = blockExclusiveScan<kThreads>(sum, red, &all);
-  if (per <= kR) {
+  for (uint32_t base = 0; base < k; base += kR * kThreads) {
+    uint32_t v[kR];
 #pragma unroll
     for (uint32_t j = 0; j < kR; ++j) {
-      if (j < mine) tc[t0 + j] = run;
-      run += v[j];
+      const uint32_t i = base + j * kThreads + threadIdx.x;
+      v[j] = i < k ? counts[i] : 0u;
     }
-  } else {
-    for (uint32_t k = 0; k < mine; k += kR) {
 #pragma unroll
-      for (uint32_t j = 0; j < kR; ++j) v[j] = k + j < mine ? tc[t0 + k + j] : 0u;
-#pragma unroll
-      for (uint32_t j = 0; j < kR; ++j) {
-        if (k + j < mine) tc[t0 + k + j] = run;
-        run += v[j];
-      }
-    }
+    for (uint32_t j = 0; j < kR; ++j) sum += v[j];
   }
-  if (total && threadIdx.x == 0) total[b] = all;
+  return blockSum<kThreads>(sum, red);
 }
 
-// s3: staged nonzeros -> their list positions.  grid (tiles, batch)
+// s2: staged nonzeros -> their list positions.  grid (tiles, batch).  The
+// tile's list offset is the sum of the element's earlier tile counts
+// (tilePrefix); the last tile also stores the list's length.
 template <int FT>
 __global__ __launch_bounds__(kThreads) void k_sparseGather(BatchDesc in, uint32_t batchOffset,
                                                            uint32_t tilesPerElem,
-                                                           const uint32_t* __restrict__ tileOff,
-                                                           const uint32_t* __restrict__ listLen,
+                                                           const uint32_t* __restrict__ tileCounts,
+                                                           uint32_t* __restrict__ listLen,
                                                            const WordOf<FT>* __restrict__ staging,
                                                            BatchDesc lists) {
   using W = WordOf<FT>;
+  __shared__ uint32_t red[kWaves];
   const uint32_t b = batchOffset + blockIdx.y;
   const uint32_t n = in.size(b);
   const uint32_t tile = blockIdx.x;
   if (tile * kTileWords >= n) return;
   const uint64_t row = uint64_t(b) * tilesPerElem + tile;
-  const uint32_t off = tileOff[row];
-  const bool lastTile = (tile + 1) * kTileWords >= n;
-  const uint32_t cnt = (lastTile ? listLen[b] : tileOff[row + 1]) - off;
+  const uint32_t cnt = tileCounts[row];
+  const uint32_t off = tilePrefix(G(tileCounts) + uint64_t(b) * tilesPerElem, tile, red);
+  if ((tile + 1) * kTileWords >= n && threadIdx.x == 0) listLen[b] = off + cnt;
   const W* st = staging + row * (kTileWords + 1);
   gp<W> list = (gp<W>)lists.start(b);
   for (uint32_t i = threadIdx.x; i < cnt; i += kThreads) list[off + i] = st[i];
-}
-
-// outSize of the sparse archive: header + padded bitmap + dense archive
-__global__ void k_sparseAddSizes(BatchDesc in, uint32_t numInBatch, uint32_t* __restrict__ outSize) {
-  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b < numInBatch && outSize) outSize[b] += 16 + roundUp((in.size(b) + 7) / 8, 16);
 }
 
 // d1: headers -> dense-archive pointers and sizes, and per-tile popcounts of
@@ -313,7 +278,7 @@ __global__ __launch_bounds__(kThreads) void k_sparseHeaders(BatchDesc in, uint32
 template <int FT, bool kVec>
 __global__ __launch_bounds__(kThreads) void k_sparseExpand(BatchDesc in, BatchDesc out, uint32_t batchOffset,
                                                            uint32_t tilesPerElem, const uint32_t* __restrict__ sizes,
-                                                           const uint32_t* __restrict__ tileOff,
+                                                           const uint32_t* __restrict__ tileCounts,
                                                            BatchDesc lists,
                                                            const uint8_t* __restrict__ denseOk,
                                                            uint8_t* __restrict__ outSuccess,
@@ -323,6 +288,7 @@ __global__ __launch_bounds__(kThreads) void k_sparseExpand(BatchDesc in, BatchDe
   constexpr uint32_t kVecs = kTileWords * sizeof(W) / 16 / kThreads;
   __shared__ __attribute__((aligned(16))) W buf[kTileWords];
   __shared__ uint32_t waveCnt[kWaves];
+  __shared__ uint32_t red[kWaves];
   const uint32_t b = batchOffset + blockIdx.y;
   const uint32_t n = sizes[b];
   const bool ok = denseOk[b] != 0 && out.size(b) >= n;
@@ -334,8 +300,6 @@ __global__ __launch_bounds__(kThreads) void k_sparseExpand(BatchDesc in, BatchDe
   }
   const uint32_t t0 = tile * kTileWords;
   if (!ok || t0 >= n) return;
-  // (issued with the bitmap loads: one memory latency fewer per tile)
-  uint32_t pos = tileOff[uint64_t(b) * tilesPerElem + tile];
   gp<const uint8_t> bm = (gp<const uint8_t>)in.start(b) + 16;
   uint64_t m[kSteps];
   uint32_t cnt = 0;
@@ -346,6 +310,9 @@ __global__ __launch_bounds__(kThreads) void k_sparseExpand(BatchDesc in, BatchDe
     if (i0 < n && n - i0 < 64) m[j] &= (1ull << (n - i0)) - 1;
     cnt += uint32_t(__popcll(m[j]));
   }
+  // the tile's first list index: the earlier tiles' popcounts (in flight
+  // together with the bitmap loads above)
+  uint32_t pos = tilePrefix(G(tileCounts) + uint64_t(b) * tilesPerElem, tile, red);
   if (lane == 0) waveCnt[w] = cnt;
   __syncthreads();
   for (uint32_t k = 0; k < w; ++k) pos += waveCnt[k];
@@ -426,19 +393,14 @@ void sparseCompressT(StackDeviceMemory& res, const FloatCompressConfig& config, 
       else launch(std::false_type{}, std::false_type{});
     }
     HIP_LAUNCH_CHECK();
-    k_sparseScan<<<ny, kThreads, 0, s>>>(y0, tiles, nullptr, in, tileCounts.data(), listLen.data());
-    HIP_LAUNCH_CHECK();
     k_sparseGather<FT><<<dim3(tiles, ny), kThreads, 0, s>>>(in, y0, tiles, tileCounts.data(), listLen.data(),
                                                              staging.data(), lists);
     HIP_LAUNCH_CHECK();
   }
   const PartialHist pre{hist.data(), R};
+  // the dense archive's writer adds the sparse header + bitmap to outSize
   floatCompressDescs(res, config, nb, lists, maxN, denseOut, outSize_dev, s, nullptr, true,
-                     countHist ? &pre : nullptr);
-  if (outSize_dev) {
-    k_sparseAddSizes<<<divUp(nb, 128), 128, 0, s>>>(in, nb, outSize_dev);
-    HIP_LAUNCH_CHECK();
-  }
+                     countHist ? &pre : nullptr, in.sizes);
 }
 
 template <int FT>
@@ -460,8 +422,6 @@ FloatDecompressStatus sparseDecompressT(StackDeviceMemory& res,
     prof::Scope p("sparse", s);
     k_sparseHeaders<<<dim3(tiles, ny), kThreads, 0, s>>>(in, y0, tiles, densePtrs.data(), sizes.data(),
                                                           tileCounts.data());
-    HIP_LAUNCH_CHECK();
-    k_sparseScan<<<ny, kThreads, 0, s>>>(y0, tiles, sizes.data(), in, tileCounts.data(), nullptr);
     HIP_LAUNCH_CHECK();
   }
   // dense decode of the nonzero list (capacity: the largest output)
