@@ -316,15 +316,20 @@ def _extras(dev, pb, reps=3):
     fams = ("compress", "hist", "normalize", "encode", "coalesce", "decode", "sparse")
 
     def breakdown(fc, fd):
-        """avg ms per launch of each kernel family in one extra profiled call
-        of each direction (event pairs around every launch)"""
+        """avg ms per launch of each kernel family over four back-to-back
+        profiled calls of each direction (event pairs around every launch)"""
         r = {}
         for tag, fn in (("c", fc), ("d", fd)):
             torch.cuda.synchronize()
             C.profile_reset()
             C.profile_filter(None)
-            C.profile(True)
+            # an unprofiled call first, so the GPU is busy while the host
+            # enqueues the profiled ones: an event pair around a launch the
+            # idle GPU waits for would time the host's launch latency too
             fn()
+            C.profile(True)
+            for _ in range(4):
+                fn()
             torch.cuda.synchronize()
             C.profile(False)
             for k in fams:
@@ -333,13 +338,35 @@ def _extras(dev, pb, reps=3):
                     r[f"{tag}:{k}"] = round(ms / launches, 4)
         return r
 
+    def roofline_of(U, C_bytes, tc, td, kern):
+        """HBM roofline of the whole call (2(U + C) over compress + decompress
+        time) and of its dominant data kernel: the family of the largest avg
+        launch time among those with algorithmic bytes (U + C for the
+        encoders and the decoder, U for the histogram pass), timed by the
+        profiled pass's event pairs (which include each launch's overhead)."""
+        call = 2 * (U + C_bytes) / ((tc + td) * 1e-3) / 1e9
+        r = {"bound": "hbm", "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+             "call_achieved": round(call, 1), "call_frac": round(call / HBM_PEAK_GBPS, 4)}
+        algo = {"compress": U + C_bytes, "encode": U + C_bytes, "decode": U + C_bytes, "hist": U}
+        # (sparse calls: the dense kernels work on the compacted list, not on
+        # U, so only the whole call is priced)
+        cand = [(ms, k[2:]) for k, ms in (kern or {}).items()
+                if k[2:] in algo and ms > 0 and "c:sparse" not in kern]
+        if cand:
+            ms, fam_ = max(cand)
+            ach = algo[fam_] / (ms * 1e-3) / 1e9
+            r.update({"kernel": KERNEL_OF[fam_], "achieved": round(ach, 1), "frac": round(ach / HBM_PEAK_GBPS, 4),
+                      "algorithmic_bytes_per_launch": algo[fam_]})
+        return r
+
     def record(name, U, C_bytes, tc, td, exact, **kw):
         out.append({"config": name, "uncompressed_bytes": U, "ratio": round(C_bytes / U, 5),
                     "compress_ms": round(tc, 3), "decompress_ms": round(td, 3),
                     "compress_GBps": round(U / tc / 1e6, 1), "decompress_GBps": round(U / td / 1e6, 1),
                     "encode_plus_decode_GBps": round(U / (tc + td) / 1e6, 1),
                     "algorithmic_GBps": round(2 * (U + C_bytes) / (tc + td) / 1e6, 1),
-                    "roundtrip_bit_exact": bool(exact), **kw})
+                    "roundtrip_bit_exact": bool(exact),
+                    "roofline": roofline_of(U, C_bytes, tc, td, kw.get("kernels_ms")), **kw})
 
     # c3: 1024 x 4 MiB bytes, uniform over 16 symbols (4.0 bit/sym)
     nb, n = 1024, 4 << 20

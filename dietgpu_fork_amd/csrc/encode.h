@@ -313,6 +313,9 @@ static __global__ __launch_bounds__(kThreads) void k_normalize(NormArgs a, uint3
 // (hs[sym * 32 + (lane & 31)]): every ds_add of a wave half hits 32
 // distinct banks and never the same address, however skewed the symbol
 // distribution (float exponents concentrate on a handful of values).
+// fp64's two segments take 16 columns each (32 KB instead of 64: four
+// workgroups per CU instead of two; c4 fp64 compress 128 -> 124 us), where
+// lanes l and l + 16 of a wave half share a column.
 // ---------------------------------------------------------------------------
 constexpr int kHistCols = 32;
 
@@ -324,6 +327,9 @@ __global__ __launch_bounds__(kThreads) void k_hist(BatchDesc in, uint32_t batchO
                                                    uint32_t* __restrict__ partCk, NormArgs na) {
   using WordT = typename FloatTraits<FT>::WordT;
   constexpr int kSegs = FloatTraits<FT>::kSegs;
+  // two segments (fp64): 16 columns each, so the counters take 32 KB and
+  // four workgroups fit a CU (64 KB allowed two)
+  constexpr int kHistCols = kSegs == 2 ? 16 : dietgpu::kHistCols;
   __shared__ __attribute__((aligned(16))) uint32_t hs[kSegs][kNumSymbols * kHistCols];
   __shared__ uint32_t red[kWaves];
 
