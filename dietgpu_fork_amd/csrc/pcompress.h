@@ -85,8 +85,11 @@ constexpr uint32_t kSpill = kRing - 128;
 // Largest team summed by every member (a 1 MiB-symbol element): its partials
 // are one sc1 load per member and bin.
 constexpr uint32_t kMaxTeam = 32;
-// histogram: u32 counters, 8 columns (lane & 7) per bin, rows padded to 9
-constexpr uint32_t kHistCols = 8;
+// histogram: u32 counters, 12 columns (l % 12 of a 32-lane half) per bin,
+// rows padded to 13: two or three lanes of a half share a column where 8
+// columns had four, so hot bins serialise less (c2 compress 143.5 -> 141.5
+// us same-box; 13.3 KB, the most that keeps four workgroups per CU)
+constexpr uint32_t kHistCols = 12;
 constexpr uint32_t kHistStride = kHistCols + 1;
 constexpr uint32_t kHistWords = 256 * kHistStride;
 }  // namespace pc
@@ -244,7 +247,7 @@ __global__ __launch_bounds__(pc::kThreads) __attribute__((amdgpu_waves_per_eu(4,
   auto tidNow = [&]() __attribute__((always_inline)) -> uint32_t { return (w << 6) + laneNow(); };
   uint32_t hv = halfNow() ? ~0u : 0u;
   asm volatile("" : "+v"(hv));  // keep `hv & x` a v_and
-  lp<uint32_t> hcol = (lp<uint32_t>)&hist[l & (pc::kHistCols - 1)];
+  lp<uint32_t> hcol = (lp<uint32_t>)&hist[l % pc::kHistCols];
   // quad byte transpose of the symbols (phase 1): lane l = 4 qm + qr
   const uint32_t qr = l & 3, qm = l >> 2;
   const uint32_t sel1 = (qr & 2) ? 0x03020706u : 0x05040100u;
@@ -523,7 +526,7 @@ __global__ __launch_bounds__(pc::kThreads) __attribute__((amdgpu_waves_per_eu(4,
     const uint32_t lane = laneNow();
     const gp<const WordT> src = (gp<const WordT>)startOf(IN(), it.b);
     const uint32_t nv = divUp(it.n, kWPV);
-    lp<uint32_t> col = (lp<uint32_t>)&hist[lane & (pc::kHistCols - 1)];
+    lp<uint32_t> col = (lp<uint32_t>)&hist[lane % pc::kHistCols];
     uint32_t x = 0;
     for (uint32_t v = lane; v < nv; v += 64) {
       const uint4 q = ld16(src + uint64_t(v) * kWPV);
