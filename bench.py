@@ -110,6 +110,9 @@ def main():
     out_ptrs = N.ptr_array([out.data_ptr() + i * n * 2 for i in range(nb)])
     caps = N.u32_array([n] * nb)
     stream = torch.cuda.current_stream(dev).cuda_stream
+    if os.environ.get("DIETGPU_BENCH_ADDRS"):  # dev: buffer placement of this process
+        print("addrs", {k: hex(t.data_ptr()) for k, t in (("x", x), ("comp", comp), ("out", out))},
+              file=sys.stderr)
 
     def step():
         N.check(L.dietgpu_float_compress(ws.h, ft, pb, 0, nb, in_ptrs, in_size, comp_ptrs,
