@@ -258,6 +258,17 @@ def test_forced_wait_timeout_poisons(C, ws):
         aout, aosz = C.ans_encode_pointer([big], ws=ws)
         agot = aosz.cpu().tolist()
         anerr = C.device_error_count(reset=True)
+        # sparse: the dense archive's size writer adds the header + bitmap,
+        # so an abandoned element keeps size 0 (not a header-sized stub)
+        g = torch.Generator(device=DEV).manual_seed(21)
+        sp = []
+        for _ in range(2):
+            f = torch.randn(600000, generator=g, device=DEV)
+            f[torch.rand(f.numel(), generator=g, device=DEV) < 0.5] = 0.0
+            sp.append(f)
+        _, spsz = C.sparse_compress(sp, ws=ws)
+        spgot = spsz.cpu().tolist()
+        spnerr = C.device_error_count(reset=True)
         with pytest.raises(RuntimeError):
             torch.ops.dietgpu.compress_data_simple(True, ts[:1], False)
         C.device_error_count(reset=True)
@@ -265,6 +276,7 @@ def test_forced_wait_timeout_poisons(C, ws):
         C.set_spin_cap(1 << 24)
     assert got == [0, 0, 0] and nerr == 3
     assert agot == [0] and anerr == 1
+    assert spgot == [0, 0] and spnerr == 2
     assert snerr == 0
     for i, w in enumerate(small):
         ref = O.float_compress(w, 2)

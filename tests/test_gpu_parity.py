@@ -265,3 +265,29 @@ def test_sparse_large_lists(C, ws, ft):
     assert ok.cpu().tolist() == [1] * len(ts)
     for w, o in zip(words, outs):
         np.testing.assert_array_equal(to_np_words(o, ft), w)
+
+
+def test_sparse_many_tiles(C, ws):
+    """One element of more than 4,096 tiles of 4,096 words: the per-tile
+    prefix of the earlier tiles' counts (k_sparseGather / k_sparseExpand,
+    16 loads in flight per thread) then takes more than one round of loads;
+    a ragged last tile and a second, one-tile element in the same batch."""
+    ft = 2
+    sizes = [4100 * 4096 + 123, 777]
+    words = [sparsify(float_words(ft, n, seed=90 + i), 0.9, seed=95 + i) for i, n in enumerate(sizes)]
+    ts = [to_dev_words(w, ft) for w in words]
+    out, osz = C.sparse_compress(ts, ft=ft, ws=ws)
+    host = out.cpu().numpy()
+    osz_h = osz.cpu().tolist()
+    for i, w in enumerate(words):
+        ref = O.sparse_compress(w, ft)
+        assert osz_h[i] == ref.size, (i, osz_h[i], ref.size)
+        np.testing.assert_array_equal(host[i, : ref.size], ref, err_msg=f"element {i}")
+    arch = [out[i, : osz_h[i]].clone() for i in range(len(ts))]
+    del out
+    outs = [torch.empty(n, dtype=TORCH_WORD[ft], device=DEV) for n in sizes]
+    ok, sz = C.sparse_decompress(arch, outs, ft=ft, ws=ws)
+    assert ok.cpu().tolist() == [1, 1]
+    assert sz.cpu().tolist() == sizes
+    for w, o in zip(words, outs):
+        np.testing.assert_array_equal(to_np_words(o, ft), w)
