@@ -126,7 +126,9 @@ XW = [("encode.h", """  uint32_t dst;
   asm volatile("s_and_saveexec_b64 %0, %1\n\tds_write_b16 %2, %3\n\ts_mov_b64 exec, %0"
                : "=&s"(sav_) : "s"(vote), "v"(ringAddr), "v"(p.x) : "memory", "scc");""")]
 VARS = {
-              (P, "lp<uint32_t> col = (lp<uint32_t>)&hist[lane & (pc::kHistCols - 1)];", "lp<uint32_t> col = (lp<uint32_t>)&hist[lane % pc::kHistCols];")],
+    "kf8": [(P, "constexpr uint32_t kFirst = 4;                         // loaded before the barrier", "constexpr uint32_t kFirst = 8;                         // loaded before the barrier")],
+    "sl0": [(P, "        if (spins) __builtin_amdgcn_s_sleep(2);", "        (void)spins;"),
+            ("lookback.h", "      __builtin_amdgcn_s_sleep(2);", "      ;")],
     "xw": XW,
     "encprio": [("encode.h", "    // every wave's slot stores are complete before other waves copy them\n    asm volatile(\"s_waitcnt vmcnt(0)\" ::: \"memory\");", "    __builtin_amdgcn_s_setprio(2);\n    // every wave's slot stores are complete before other waves copy them\n    asm volatile(\"s_waitcnt vmcnt(0)\" ::: \"memory\");")],
     "d3": [(P, "  constexpr int D = 2;", "  constexpr int D = 3;")],
