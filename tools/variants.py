@@ -126,6 +126,9 @@ XW = [("encode.h", """  uint32_t dst;
   asm volatile("s_and_saveexec_b64 %0, %1\n\tds_write_b16 %2, %3\n\ts_mov_b64 exec, %0"
                : "=&s"(sav_) : "s"(vote), "v"(ringAddr), "v"(p.x) : "memory", "scc");""")]
 VARS = {
+    "dp1": [("codec.hip", "constexpr uint32_t kMaxDecodeChunks = 8;", "constexpr uint32_t kMaxDecodeChunks = 1;")],
+    "dc4": [("codec.hip", "constexpr uint32_t kMaxDecodeChunks = 8;", "constexpr uint32_t kMaxDecodeChunks = 4;")],
+    "dc16": [("codec.hip", "constexpr uint32_t kMaxDecodeChunks = 8;", "constexpr uint32_t kMaxDecodeChunks = 16;")],
     "kf8": [(P, "constexpr uint32_t kFirst = 4;                         // loaded before the barrier", "constexpr uint32_t kFirst = 8;                         // loaded before the barrier")],
     "sl0": [(P, "        if (spins) __builtin_amdgcn_s_sleep(2);", "        (void)spins;"),
             ("lookback.h", "      __builtin_amdgcn_s_sleep(2);", "      ;")],
