@@ -126,6 +126,8 @@ XW = [("encode.h", """  uint32_t dst;
   asm volatile("s_and_saveexec_b64 %0, %1\n\tds_write_b16 %2, %3\n\ts_mov_b64 exec, %0"
                : "=&s"(sav_) : "s"(vote), "v"(ringAddr), "v"(p.x) : "memory", "scc");""")]
 VARS = {
+    "hcl": [(P, "lp<uint32_t> hcol = (lp<uint32_t>)&hist[l % pc::kHistCols];", "lp<uint32_t> hcol = (lp<uint32_t>)&hist[laneNow() % pc::kHistCols];")],
+    "hcx": [(P, "lp<uint32_t> hcol = (lp<uint32_t>)&hist[l % pc::kHistCols];", "lp<uint32_t> hcol = (lp<uint32_t>)&hist[(l + (halfNow() ? 6u : 0u)) % pc::kHistCols];")],
     "dp1": [("codec.hip", "constexpr uint32_t kMaxDecodeChunks = 8;", "constexpr uint32_t kMaxDecodeChunks = 1;")],
     "dc4": [("codec.hip", "constexpr uint32_t kMaxDecodeChunks = 8;", "constexpr uint32_t kMaxDecodeChunks = 4;")],
     "dc16": [("codec.hip", "constexpr uint32_t kMaxDecodeChunks = 8;", "constexpr uint32_t kMaxDecodeChunks = 16;")],
