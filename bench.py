@@ -199,6 +199,20 @@ def main():
     torch.cuda.synchronize()
     C.profile(False)
     breakdown = query_families()
+    # decode from HBM-sourced archives: the step above
+    # decodes archives the compressor has just written, most of which are
+    # still in the 256 MiB Infinity Cache (MALL).  Here, after each compress,
+    # a 512 MiB fill evicts them before the decode is timed alone; the same
+    # isolated timing without the fill is the warm figure.  Untimed for the
+    # headline, which stays the reference's compress -> decompress loop.
+    decode_cold = None if world > 1 else _decode_cold_warm(step_parts=(
+        lambda: N.check(L.dietgpu_float_compress(ws.h, ft, pb, 0, nb, in_ptrs, in_size, comp_ptrs,
+                                                 sizes.data_ptr(), stream)),
+        lambda: N.check(L.dietgpu_float_decompress(ws.h, ft, pb, 0, nb, comp_ptrs, out_ptrs, caps,
+                                                   ok.data_ptr(), osz.data_ptr(), stream))), dev=dev)
+    if args.verify:
+        torch.cuda.synchronize()
+        assert torch.equal(out.view(torch.int16), x.view(torch.int16)), "roundtrip mismatch (cold decode)"
     elapsed = t1 - t0
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -222,10 +236,12 @@ def main():
     roofline = None
     if dominant:
         ach = algo[dominant] / (fam[dominant]["avg_ms"] * 1e-3) / 1e9
+        # PMC traffic is profiled on c2 (tools/profile_gpu.sh) for one build of
+        # the library: taken only from a summary of THIS build (its sha256)
+        traffic, tsrc = _pmc_traffic(dominant, ft) if workload == "c2" else (None, None)
         roofline = {"bound": "hbm", "kernel": KERNEL_OF[dominant], "achieved": round(ach, 1),
                     "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBPS, 4),
-                    # PMC traffic is profiled on c2 (tools/profile_gpu.sh)
-                    "traffic": _pmc_traffic(dominant, ft) if workload == "c2" else None,
+                    "traffic": traffic, "traffic_source": tsrc,
                     "algorithmic_bytes_per_launch": algo[dominant]}
     t_enc = sum(fam[k]["avg_ms"] for k in ("compress", "hist", "normalize", "encode", "coalesce") if k in fam)
     t_dec = fam.get("decode", {}).get("avg_ms", 0.0)
@@ -253,6 +269,19 @@ def main():
         "roofline": roofline,
         "cpu_baseline": None,
     }
+    if decode_cold:
+        # the step with the decode reading its archives from HBM: the timed
+        # step's own decode replaced by the isolated cold one
+        t_hot, t_cold = decode_cold["decode_warm_ms"], decode_cold["decode_cold_ms"]
+        dec_live = fam.get("decode", {}).get("avg_ms", t_hot)
+        step_cold = ms_per_step - dec_live + t_cold
+        decode_cold.update({
+            "step_cold_ms": round(step_cold, 4),
+            "encode_plus_decode_algorithmic_GBps_cold": round(2 * (U + comp_bytes) / (step_cold * 1e-3) / 1e9, 1),
+            "decode_cold_algorithmic_GBps": round((U + comp_bytes) / (t_cold * 1e-3) / 1e9, 1),
+            "decode_warm_algorithmic_GBps": round((U + comp_bytes) / (t_hot * 1e-3) / 1e9, 1)})
+        line["decode_hbm"] = decode_cold
+        line["encode_plus_decode_algorithmic_GBps_step"] = round(2 * (U + comp_bytes) / (ms_per_step * 1e-3) / 1e9, 1)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = _cpu_baseline(x, min(args.cpu_sample, nb), pb)
     if world == 1 and workload == "c2" and args.extras:
@@ -280,6 +309,36 @@ def _bf16_rows(first, last, n, dev, chunk=512):
         x[a - first:b - first] = rows.view(torch.bfloat16)
         del x32
     return x
+
+
+def _decode_cold_warm(step_parts, dev, reps=8, flush_bytes=512 << 20):
+    """Isolated decode times (torch events on the launch stream): `warm`
+    right after a compress (archives partly in the MALL, as in the timed
+    step), `cold` after a compress and a flush_bytes fill that evicts them
+    (the decoder then reads its archives from HBM)."""
+    import torch
+
+    compress, decompress = step_parts
+    scratch = torch.empty(flush_bytes, dtype=torch.uint8, device=dev)
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    res = {}
+    for name, flush in (("warm", False), ("cold", True)):
+        tot = 0.0
+        for i in range(reps + 1):
+            compress()
+            if flush:
+                scratch.fill_(i & 0xFF)
+            a.record()
+            decompress()
+            b.record()
+            b.synchronize()
+            if i:  # the first of each kind untimed
+                tot += a.elapsed_time(b)
+        res[f"decode_{name}_ms"] = round(tot / reps, 5)
+    del scratch
+    res["note"] = (f"decode timed alone after a compress; cold: a {flush_bytes >> 20} MiB fill between them "
+                   "evicts the archives from the 256 MiB Infinity Cache")
+    return res
 
 
 def _timed(fn, reps, min_ms=2.0, max_reps=50):
@@ -493,13 +552,28 @@ KERNEL_OF = {"compress": "k_pcompress", "hist": "k_hist", "normalize": "k_normal
              "coalesce": "k_coalesce", "decode": "k_decode", "sparse": "k_sparse"}
 
 
+def library_sha256():
+    """sha256 of the HIP library this process runs (dietgpu_fork_amd/_lib)."""
+    import hashlib
+
+    p = os.path.join(ROOT, "dietgpu_fork_amd", "_lib", "libdietgpu_amd.so")
+    try:
+        return hashlib.sha256(open(p, "rb").read()).hexdigest()
+    except OSError:
+        return None
+
+
 def _pmc_traffic(kernel, ft):
-    """HBM bytes per launch of `kernel`'s instance for float type `ft` from
-    the newest committed rocprofv3 PMC summary (profiles/*pmc*.json, written
-    by tools/pmc_summary.py, keyed per template instance), or None."""
+    """(HBM bytes per launch, source file) of `kernel`'s instance for float
+    type `ft` from the newest committed rocprofv3 PMC summary
+    (profiles/*pmc*.json, written by tools/pmc_summary.py, keyed per template
+    instance) that was collected on THIS build of the library (its
+    library_sha256): counters of another build would silently describe other
+    code.  (None, reason) when there is none."""
     def natural(f):  # r01_v10 after r01_v9
         return [int(t) if t.isdigit() else t for t in re.split(r"(\d+)", os.path.basename(f))]
 
+    lib = library_sha256()
     # newest summary first; within a round the profile of the driver's own
     # command (profiles/rNN_driver_cmd_pmc.json) before the others
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")),
@@ -509,10 +583,12 @@ def _pmc_traffic(kernel, ft):
             d = json.load(open(f))
         except Exception:
             continue
+        if lib is None or d.get("library_sha256") != lib:
+            continue
         for name, k in d.get("kernels", {}).items():
             if name.startswith(f"{KERNEL_OF[kernel]}<{ft},") and "hbm_bytes_per_launch" in k:
-                return k["hbm_bytes_per_launch"]
-    return None
+                return k["hbm_bytes_per_launch"], os.path.relpath(f, ROOT)
+    return None, "no committed PMC summary of this library build (sha256 %s)" % (lib or "?")[:16]
 
 
 def _cpu_baseline(x, sample, pb, min_seconds=12.0, max_passes=40):

@@ -39,7 +39,9 @@ def _declare(L):
         "dietgpu_device_error_count": (c_u32, [c_int]),
         "dietgpu_set_spin_cap": (None, [c_u32]),
         "dietgpu_set_barrier_budget": (None, [c_u32]),
+        "dietgpu_set_dispatch_skew": (None, [c_u32]),
         "dietgpu_test_occupy": (c_int, [P, c_u32, c_u32, c_u32]),
+        "dietgpu_test_histogram": (c_int, [vp, c_u32, P, c_u32, c_u32, P, P]),
         "dietgpu_version": (ctypes.c_char_p, []),
         "dietgpu_stack_create": (vp, [c_int, P, c_size]),
         "dietgpu_stack_destroy": (None, [vp]),
@@ -83,7 +85,7 @@ def _declare(L):
                                           ctypes.POINTER(ctypes.c_uint64)]),
     }
     # test hooks absent from older builds (same-box A/B of earlier libraries)
-    optional = {"dietgpu_set_barrier_budget", "dietgpu_test_occupy"}
+    optional = {"dietgpu_set_barrier_budget", "dietgpu_set_dispatch_skew", "dietgpu_test_occupy", "dietgpu_test_histogram"}
     for name, (res, args) in sig.items():
         if name in optional and not hasattr(L, name):
             continue

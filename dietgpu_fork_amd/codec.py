@@ -34,6 +34,17 @@ def _ws(ws, device):
     return ws if ws is not None else Workspace(256, device)
 
 
+def test_histogram(x2d, size=None, ws=None):
+    """Test hook: per-row byte histograms of a [nb, stride] uint8 CUDA tensor
+    (the first `size` bytes of each row) by the compressor's histogram kernel."""
+    nb, stride = x2d.shape
+    size = stride if size is None else size
+    hist = torch.empty([nb, 256], dtype=torch.int32, device=x2d.device)
+    ws = _ws(ws, x2d.device)
+    N.check(N.lib().dietgpu_test_histogram(ws.h, nb, x2d.data_ptr(), size, stride, hist.data_ptr(), _s()))
+    return hist
+
+
 def max_compressed_size(nbytes):
     return N.size_or_raise(N.lib().dietgpu_get_max_compressed_size(int(nbytes)))
 
@@ -51,6 +62,11 @@ def device_error_count(reset=True):
     """Elements the compressor abandoned (outSize 0) since the last reset;
     synchronises the device."""
     return int(N.lib().dietgpu_device_error_count(int(reset)))
+
+
+def set_dispatch_skew(ticks):
+    """Test hook: emulate out-of-order workgroup dispatch (0 = off)."""
+    N.lib().dietgpu_set_dispatch_skew(int(ticks))
 
 
 def set_spin_cap(polls):

@@ -17,6 +17,8 @@ using namespace dietgpu;
 
 namespace dietgpu {
 void testOccupy(hipStream_t s, uint32_t micros, uint32_t workgroups, uint32_t ldsBytes);
+void testHistogram(StackDeviceMemory& res, hipStream_t s, uint32_t nb, const void* in_dev, uint32_t size,
+                   uint32_t stride, uint32_t* hist_dev);
 }
 
 struct dietgpu_stack {
@@ -308,10 +310,19 @@ uint32_t dietgpu_device_error_count(int reset) {
 
 void dietgpu_set_spin_cap(uint32_t polls) { setSpinCap(polls); }
 void dietgpu_set_barrier_budget(uint32_t ticks) { setBarrierBudget(ticks); }
+void dietgpu_set_dispatch_skew(uint32_t ticks) { setDispatchSkew(ticks); }
 
 int dietgpu_test_occupy(void* stream, uint32_t micros, uint32_t workgroups, uint32_t lds_bytes) {
   return guarded([&] {
     testOccupy(S(stream), micros, workgroups, lds_bytes);
+    return DIETGPU_OK;
+  });
+}
+
+int dietgpu_test_histogram(dietgpu_stack* res, uint32_t nb, const void* in_dev, uint32_t size,
+                           uint32_t stride, uint32_t* hist_dev, void* stream) {
+  return guarded([&] {
+    testHistogram(R(res), S(stream), nb, in_dev, size, stride, hist_dev);
     return DIETGPU_OK;
   });
 }

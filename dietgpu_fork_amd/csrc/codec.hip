@@ -237,7 +237,7 @@ bool compressPersistent(StackDeviceMemory& res, int pb, bool useChecksum, uint32
   const uint32_t maxR = 2 * divUp(nb, teams) + 2;
   const size_t regions[kSyncRegions] = {16, size_t(items) * 8, partBytes + (kCk ? size_t(items) * 4 : 0),
                                         size_t(teams) * maxR * 8, 0};
-  SyncLease lease(res, s, regions);
+  SyncLease lease(res, s, regions, /*dequeue=*/true);
   if (FT != 0 && useChecksum) {
     HIP_CHECK(hipMemsetAsync(ck.data(), 0, sizeof(uint32_t) * nb, s));
     // float checksum: the reference passes float-word counts as byte counts
@@ -272,6 +272,8 @@ bool compressPersistent(StackDeviceMemory& res, int pb, bool useChecksum, uint32
   a.epoch = lease.epoch;
   a.spinCap = spinCap();
   a.fallbackTicks = barrierBudgetTicks();
+  a.ticket = lease.ticket();
+  a.skew = dispatchSkew();
   a.pb = pb;
   a.useChecksum = useChecksum;
   prof::Scope p("compress", s);
@@ -295,6 +297,7 @@ void encodeBatchDevice(StackDeviceMemory& res, int pb, bool useChecksum, uint32_
   const uint32_t MB = divUp(maxSize, kBlockSize);
   const bool userHist = FT == 0 && hist_dev != nullptr;
   const bool preHist = FT != 0 && pre != nullptr;  // partial rows counted by the caller
+  const bool preNorm = preHist && pre->table != nullptr;  // ... and normalised
   const uint32_t chunkWords = histChunkWords(nb, maxSize);
   const uint32_t chunks = preHist ? std::max(1u, pre->nRows) : std::max(1u, divUp(maxSize, chunkWords));
   const bool runHist = !preHist && (!userHist || useChecksum);
@@ -317,16 +320,17 @@ void encodeBatchDevice(StackDeviceMemory& res, int pb, bool useChecksum, uint32_
   const uint32_t* chunkRows = preHist ? pre->rows : partHist.data();
   // first-level sums when elements have many chunks (k_histReduce)
   const uint32_t groups = divUp(chunks, kReduceRows);
-  const bool reduce2 = (runHist || preHist) && chunks > kReduceRows;
+  const bool reduce2 = (runHist || preHist) && !preNorm && chunks > kReduceRows;
   auto groupHist = res.alloc<uint32_t>(s, reduce2 ? size_t(kSegs) * nb * groups * kNumSymbols : 1);
   auto groupCk = res.alloc<uint32_t>(s, reduce2 && rawCk ? size_t(nb) * groups : 1);
   auto ck = res.alloc<uint32_t>(s, nb);
-  auto table = res.alloc<uint4>(s, size_t(kSegs) * nb * kNumSymbols);
-  auto pdf = res.alloc<uint16_t>(s, size_t(kSegs) * nb * kNumSymbols);
+  auto tableMem = res.alloc<uint4>(s, preNorm ? 1 : size_t(kSegs) * nb * kNumSymbols);
+  auto pdfMem = res.alloc<uint16_t>(s, preNorm ? 1 : size_t(kSegs) * nb * kNumSymbols);
+  const uint4* table = preNorm ? pre->table : tableMem.data();
+  const uint16_t* pdf = preNorm ? pre->pdf : pdfMem.data();
   auto slots = res.alloc<uint8_t>(s, size_t(kSegs) * nb * std::max(MB, 1u) * kSlotBytes);
   auto cw = res.alloc<uint32_t>(s, kFused ? 1 : size_t(kSegs) * nb * std::max(MB, 1u));
   const uint32_t nW = std::max(1u, divUp(MB, EncCfg<FT>::kBlocksPerWG));
-  auto flags = res.alloc<uint64_t>(s, kFused ? size_t(nb) * nW : 1);
   // the normalisation runs in the last workgroup of the kernel that writes
   // an element's final partial rows (k_histReduce, or a k_hist of at most
   // 4096 workgroups), saving the k_normalize launch.  Each of those
@@ -335,20 +339,21 @@ void encodeBatchDevice(StackDeviceMemory& res, int pb, bool useChecksum, uint32_
   // launch (c3 hist 0.74 -> 1.09 ms), so k_normalize runs there.
   const bool finalInReduce = reduce2;
   const bool finalInHist = !reduce2 && runHist && uint64_t(chunks) * nb <= 4096;
-  const size_t regions[kSyncRegions] = {0, 0, 0, 0, size_t(nb) * 4};
+  // k_encode's look-back flags (fused formats: one per element and encode
+  // workgroup, epoch-tagged, never zeroed), the start-ticket counter and the
+  // last-arrival counters, in this stream's sync arena
+  const size_t regions[kSyncRegions] = {0, kFused ? size_t(nb) * nW * 8 : 0, 0, 0, size_t(nb) * 4};
   SyncLease lease(res, s, regions);
   NormArgs na;
   na.in = in;
   na.hist = userHist ? hist_dev : (reduce2 ? groupHist.data() : chunkRows);
   na.rows = userHist ? 1u : (reduce2 ? groups : chunks);
   na.pb = pb;
-  na.table = table.data();
-  na.pdf = pdf.data();
+  na.table = tableMem.data();
+  na.pdf = pdfMem.data();
   na.partCk = rawCk ? (reduce2 ? groupCk.data() : partCk.data()) : nullptr;
   na.ckRows = reduce2 ? groups : chunks;
   na.ckOut = ck.data();
-  na.flags = kFused ? flags.data() : nullptr;
-  na.nW = nW;
   na.arrive = nullptr;
   NormArgs naFinal = na;
   naFinal.arrive = static_cast<uint32_t*>(lease.base[kSyncArrive]);
@@ -387,7 +392,7 @@ void encodeBatchDevice(StackDeviceMemory& res, int pb, bool useChecksum, uint32_
                                           finalInReduce ? naFinal : na, kSegs);
       HIP_LAUNCH_CHECK();
     }
-    if (!finalInReduce && !finalInHist) {
+    if (!finalInReduce && !finalInHist && !preNorm) {
       prof::Scope p("normalize", s);
       dim3 g(ny, kSegs);
       k_normalize<<<g, kThreads, 0, s>>>(na, y0, nb);
@@ -396,9 +401,13 @@ void encodeBatchDevice(StackDeviceMemory& res, int pb, bool useChecksum, uint32_
     if (MB > 0 || kFused) {
       prof::Scope p("encode", s);
       dim3 g(nW, ny);
-      const EncTail tail{pdf.data(), ck.data(), outSize_dev, flags.data(), nW, pb, useChecksum,
-                         spinCap(), deviceErrorWord(), sparseN};
-      k_encode<FT, 0><<<g, enc::kThreads, 0, s>>>(in, out, y0, nb, std::max(MB, 1u), table.data(),
+      EncTail tail{pdf, ck.data(), outSize_dev,
+                   kFused ? static_cast<uint64_t*>(lease.base[kSyncFlags]) : nullptr, nW, pb, useChecksum,
+                   spinCap(), deviceErrorWord(), sparseN};
+      tail.epoch = lease.epoch;
+      tail.ticket = kFused ? lease.ticket() : nullptr;
+      tail.skew = dispatchSkew();
+      k_encode<FT, 0><<<g, enc::kThreads, 0, s>>>(in, out, y0, nb, std::max(MB, 1u), table,
                                                slots.data(), cw.data(), tail);
       HIP_LAUNCH_CHECK();
     }
@@ -407,7 +416,7 @@ void encodeBatchDevice(StackDeviceMemory& res, int pb, bool useChecksum, uint32_
       const uint32_t bpw = 32;
       dim3 g(std::max(1u, divUp(MB, bpw)), ny, kSegs);
       k_coalesce<FT><<<g, kThreads, 0, s>>>(in, out, y0, nb, std::max(MB, 1u), bpw, slots.data(),
-                                            cw.data(), pdf.data(), pb, useChecksum, ck.data(),
+                                            cw.data(), pdf, pb, useChecksum, ck.data(),
                                             outSize_dev, sparseN);
       HIP_LAUNCH_CHECK();
     }

@@ -17,6 +17,7 @@
 #include <type_traits>
 
 #include "device.h"
+#include "sync_arena.h"
 
 namespace dietgpu {
 
@@ -228,17 +229,14 @@ struct NormArgs {
   const uint32_t* partCk;       // [nb][ckRows] byte-checksum partials, or null
   uint32_t ckRows;
   uint32_t* ckOut;
-  uint64_t* flags;              // k_encode's look-back flags ([nb][nW]), or null
-  uint32_t nW;
   uint32_t* arrive;             // [nb] last-arrival counters (self-resetting), or null
+  bool totalFromHist = false;   // the symbol total is the rows' sum (in.size unknown yet: sparse lists)
 };
 
 __device__ __forceinline__ void normalizeElement(const NormArgs& a, uint32_t numInBatch, uint32_t b,
                                                  uint32_t seg, uint32_t* keys, uint32_t* red, u32x4* red4) {
   const uint32_t s = threadIdx.x;
   const uint64_t row = uint64_t(seg) * numInBatch + b;
-  if (a.flags && seg == 0)  // k_encode's look-back flags (EncTail)
-    for (uint32_t i = s; i < a.nW; i += kThreads) G(a.flags)[uint64_t(b) * a.nW + i] = 0;
   // (arrive set: the last arrival of this launch, rows and checksum
   // partials handed off with sc1 stores, read with sc1 loads)
   const bool sc1 = a.arrive != nullptr;
@@ -253,7 +251,7 @@ __device__ __forceinline__ void normalizeElement(const NormArgs& a, uint32_t num
   gp<const uint32_t> rowsBase = G(a.hist) + row * a.rows * kNumSymbols;
   const uint32_t count = sc1 ? sumRows256<true>(rowsBase, a.rows, red4) : sumRows256<false>(rowsBase, a.rows, red4);
 
-  const uint32_t total = a.in.size(b);
+  const uint32_t total = a.totalFromHist ? blockSum<kThreads>(count, red) : a.in.size(b);
   if (total == 0) {  // :193-195 (the reference leaves the table untouched)
     st16(G(a.table) + row * kNumSymbols + s, make_uint4(0, 0, 0, 0));
     G(a.pdf)[row * kNumSymbols + s] = 0;
@@ -757,8 +755,8 @@ __device__ __forceinline__ void copyPayload(const uint32_t* pre, const uint32_t*
 // ---------------------------------------------------------------------------
 // Fused coalesce (single-segment formats).  Each encode workgroup publishes
 // its blocks' word total and finds its archive offset by a decoupled
-// look-back over the element's earlier workgroups (lower blockIdx.x, so
-// dispatched earlier: waiting on them cannot deadlock), then writes its own
+// look-back over the element's earlier workgroups (lower start tickets, so
+// already running: waiting on them cannot deadlock), then writes its own
 // blocks' blockWords and payload.  One 8 B flag per (element, workgroup),
 // zeroed by k_normalize: bits 63:62 = 1 aggregate / 2 inclusive prefix, low
 // 32 bits the value.  The value lives in the flag word itself, so a relaxed
@@ -778,6 +776,12 @@ struct EncTail {
   // sparse archives: element sizes whose header + bitmap precede this dense
   // archive (sparseOverhead), added to outSize; null otherwise
   const uint32_t* sparseN = nullptr;
+  // start tickets (takeTicket, device.h) of the fused path's look-back: the
+  // workgroup's (chunk, element) comes from its ticket, so the workgroups it
+  // waits on have started; null: blockIdx (no look-back, fp64)
+  uint32_t* ticket = nullptr;
+  uint32_t skew = 0;  // test hook (takeTicket)
+  uint32_t epoch = 0;  // this call's epoch: the flags are epoch-tagged (sync arena), never zeroed
 };
 
 // bytes of a sparse archive before its dense part: 16 B header, bitmap
@@ -790,18 +794,21 @@ constexpr uint64_t kFlagAgg = 1ull << 62;
 constexpr uint64_t kFlagPrefix = 2ull << 62;
 constexpr uint64_t kFlagPoisonE = 1ull << 61;
 
-// Called by one whole wave; returns (wave-uniform) the sum of the values of
-// workgroups [0, x) of the element.  Predecessors were dispatched earlier, so
-// the wait is short; if it runs out of polls (`cap`) the flag chain is
-// POISONED instead (bit 61, carried forward by every later prefix) and
-// `poison` says whether any workgroup [0, x] of the element is poisoned: the
-// last one then writes outSize = 0 rather than a wrong archive.
-__device__ __forceinline__ uint32_t lookBack(gp<uint64_t> f, uint32_t x, uint32_t agg, uint32_t cap,
-                                             bool& poison) {
+// Decoupled look-back over earlier members [0, x) (lower start tickets) of
+// an element, with epoch-tagged, poison-carrying flags: bits 63:62 status (1 aggregate, 2
+// inclusive prefix), 61 poison, 47:32 epoch, 31:0 value.  A flag of another
+// epoch reads as "not yet published".  Whole wave; returns the sum of the
+// values of members [0, x); `poison` in: this member's own, out: whether any
+// member [0, x] is poisoned (or the wait ran out of polls).
+// (storeOwn = false: this member's aggregate flag is already published)
+__device__ __forceinline__ uint32_t lookBackPoison(gp<uint64_t> f, uint32_t x, uint32_t agg,
+                                                   uint32_t epoch, uint32_t cap, bool& poison,
+                                                   bool storeOwn = true) {
   const uint32_t lane = laneId();
-  poison = false;
-  if (lane == 0)
-    __hip_atomic_store((uint64_t*)f + x, (x == 0 ? kFlagPrefix : kFlagAgg) | agg, __ATOMIC_RELAXED,
+  const uint64_t tag = uint64_t(epoch) << 32;
+  const uint64_t own = poison ? kFlagPoisonE : 0ull;
+  if (storeOwn && lane == 0)
+    __hip_atomic_store(f + x, (x == 0 ? kFlagPrefix : kFlagAgg) | own | tag | agg, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
   if (x == 0) return 0;
   uint32_t excl = 0;
@@ -810,10 +817,12 @@ __device__ __forceinline__ uint32_t lookBack(gp<uint64_t> f, uint32_t x, uint32_
   int32_t j = int32_t(x);
   for (uint32_t spins = 0; spins < cap;) {
     const int32_t k = j - 1 - int32_t(lane);
-    const uint64_t v = k >= 0 ? __hip_atomic_load((uint64_t*)f + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                              : kFlagPrefix;
-    const uint64_t isPre = ballot((v >> 63) != 0);
-    const uint64_t isZero = ballot((v >> 62) == 0);
+    const uint64_t v = k >= 0 ? __hip_atomic_load(f + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                              : (kFlagPrefix | tag);
+    const uint32_t hi = uint32_t(v >> 32);
+    const uint32_t status = (hi & kEpochMask) == epoch ? hi >> 30 : 0u;
+    const uint64_t isPre = ballot(status == 2);
+    const uint64_t isZero = ballot(status == 0);
     const uint32_t firstPre = isPre ? uint32_t(__builtin_ctzll(isPre)) : 64u;
     const uint64_t need = firstPre >= 63 ? ~0ull : (2ull << firstPre) - 1;
     if (isZero & need) {
@@ -829,10 +838,9 @@ __device__ __forceinline__ uint32_t lookBack(gp<uint64_t> f, uint32_t x, uint32_
     }
     j -= 64;
   }
-  poison = pz != 0 || !done;
+  poison = poison || pz != 0 || !done;
   if (lane == 0)
-    __hip_atomic_store((uint64_t*)f + x,
-                       kFlagPrefix | (poison ? kFlagPoisonE : 0ull) | uint64_t(excl + agg),
+    __hip_atomic_store(f + x, kFlagPrefix | (poison ? kFlagPoisonE : 0ull) | tag | uint64_t(excl + agg),
                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   return excl;
 }
@@ -919,14 +927,26 @@ __global__ __launch_bounds__(enc::kThreads) void k_encode(BatchDesc in, BatchDes
   __shared__ uint32_t cwE[Cfg::kBlocksPerWG];
   __shared__ uint32_t flE[Cfg::kBlocksPerWG];
   __shared__ uint32_t preE[Cfg::kBlocksPerWG];
+  __shared__ uint32_t ticketS;
 
-  const uint32_t b = batchOffset + blockIdx.y;
   const uint32_t tid = threadIdx.x;
+  // (chunk, element) of this workgroup: from its start ticket when it takes
+  // part in a look-back (chunk-major over the launch, as the hardware would
+  // dispatch it), so every workgroup it waits on has already started
+  uint32_t wx = blockIdx.x, wy = blockIdx.y;
+  if (kFused && tail.ticket) {
+    if (tid == 0) ticketS = takeTicket(tail.ticket, gridDim.x * gridDim.y, tail.skew);
+    __syncthreads();
+    const uint32_t t = readfirst(ticketS);
+    wy = t / gridDim.x;
+    wx = t - wy * gridDim.x;
+  }
+  const uint32_t b = batchOffset + wy;
   const uint32_t n = in.size(b);
   const uint32_t nBlocks = divUp(n, kBlockSize);
-  const uint32_t first = blockIdx.x * Cfg::kBlocksPerWG;
+  const uint32_t first = wx * Cfg::kBlocksPerWG;
   // workgroup 0 of an element always runs (headers, empty elements)
-  if (first >= nBlocks && (!kFused || blockIdx.x != 0)) return;
+  if (first >= nBlocks && (!kFused || wx != 0)) return;
   gp<uint8_t> base = startOf(out, b);
   gp<uint8_t> o = base + (FT == 0 ? 0u : 32u + floatRawBytes(FT, n));  // ANS archive
   gp<uint8_t> states = o + kANSHeaderBytes + kPdfBytes;
@@ -1136,8 +1156,8 @@ __global__ __launch_bounds__(enc::kThreads) void k_encode(BatchDesc in, BatchDes
       const uint32_t r = lane < nk ? roundUp(cwE[lane], 8) : 0u;
       const uint32_t inc = waveInclusiveScan(r);
       const uint32_t agg = readfirst(__shfl(inc, 63));
-      bool pz;
-      const uint32_t excl = lookBack(G(tail.flags) + uint64_t(b) * tail.nW, blockIdx.x, agg, tail.spinCap, pz);
+      bool pz = false;
+      const uint32_t excl = lookBackPoison(G(tail.flags) + uint64_t(b) * tail.nW, wx, agg, tail.epoch, tail.spinCap, pz);
       if (lane < nk) preE[lane] = excl + inc - r;
       if (lane == 0 && (first + Cfg::kBlocksPerWG >= nBlocks)) {
         if (pz) {
@@ -1148,7 +1168,7 @@ __global__ __launch_bounds__(enc::kThreads) void k_encode(BatchDesc in, BatchDes
         }
       }
     }
-    if (blockIdx.x == 0) writeHeadFixed<FT>(base, o, n, nBlocks, tail, b);
+    if (wx == 0) writeHeadFixed<FT>(base, o, n, nBlocks, tail, b);
     __syncthreads();
     if (tid < nk) {
       const uint32_t k = first + tid;

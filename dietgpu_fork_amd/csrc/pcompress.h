@@ -13,11 +13,9 @@
 // block pair per wave); the items of an element form its team.  The grid is
 // at most one generation of resident workgroups, a whole number of teams of
 // workgroups, and a workgroup team takes one element per round: member x of
-// team T works item x of the team's element.  Team membership keeps each
-// team on one XCD (workgroups w, w + 8, ... share one under the observed
-// round-robin placement), so the team's hand-offs stay in one L2 (speed
-// only, never correctness), and gives the members increasing workgroup
-// indices.  Elements of rounds 0 and 1 are static (r * teams + T); from
+// team T works item x of the team's element.  Workgroups are numbered by
+// start ticket (vb, see below); member x of team T has a higher ticket than
+// members 0 .. x-1.  Elements of rounds 0 and 1 are static (r * teams + T); from
 // round 2 on, member 0 takes the team's element two rounds ahead with one
 // returning add on a per-call counter and logs it (epoch-tagged) for the
 // other members, so teams that ran fast take more elements.  One add per
@@ -49,10 +47,12 @@
 // (its members have higher as well as lower indices); it is bounded by a time
 // budget (PCompArgs::fallbackTicks), after which the workgroup counts L's
 // element itself from the input (an extra read on this slow path only) and
-// goes on.  Every other wait is the look-back on LOWER members of E's team,
-// i.e. lower workgroup indices of the same round, dispatched before this one
-// (in-order dispatch) and, by induction over rounds and member index, never
-// waiting on a workgroup that is not resident.  Another kernel holding CUs
+// goes on.  Every other wait is the look-back on LOWER members of E's team.
+// Members are numbered by START TICKET (takeTicket, device.h: one atomic per
+// workgroup at its start), not by blockIdx, so a lower member is a workgroup
+// that had already started when this one took its ticket: whatever order the
+// hardware dispatches in (MI355X_MICROARCH.md: undefined), no wait is ever on
+// a workgroup that is not resident (by induction over rounds and members).  Another kernel holding CUs
 // (a second compress on another stream, an RCCL collective) therefore delays
 // the call but cannot stall it.  The look-back is still bounded by a poll cap
 // (a kernel argument); a look-back that runs out POISONS the element instead
@@ -112,10 +112,12 @@ struct PCompArgs {
   uint64_t* ctr;         // [2] element dequeue counters, this call's at epoch & 1 (sync arena)
   uint64_t* elog;        // [teams][maxR] element of each team's round, epoch << 32 | element (sync arena)
   uint32_t maxR;         // rounds a team may take
-  uint32_t slotSpan;     // workgroups per dispatch slot (the CU count): slot = blockIdx / slotSpan
+  uint32_t slotSpan;     // workgroups per dispatch slot (the CU count): slot ~ ticket / slotSpan
   uint32_t epoch;
   uint32_t spinCap;      // polls per look-back before poisoning
   uint32_t fallbackTicks;  // team-barrier wait (100 MHz ticks) before counting the element itself
+  uint32_t* ticket;      // start-ticket counter (takeTicket, device.h; sync arena)
+  uint32_t skew;         // test hook: emulated out-of-order dispatch (takeTicket)
   int pb;
   bool useChecksum;
 };
@@ -222,9 +224,16 @@ __global__ __launch_bounds__(pc::kThreads) __attribute__((amdgpu_waves_per_eu(4,
   __shared__ __attribute__((aligned(16))) uint32_t cwE[pc::kBlocksPerItem];
   __shared__ __attribute__((aligned(16))) uint32_t flE[pc::kBlocksPerItem];
   __shared__ __attribute__((aligned(16))) uint32_t preE[pc::kBlocksPerItem];
-  __shared__ uint32_t poisonS, sigS, fbS;
+  __shared__ uint32_t poisonS, sigS, fbS, vbS;
 
   const uint32_t tid = threadIdx.x;
+  // This workgroup's place in the grid is its START TICKET, not blockIdx.x:
+  // team membership, member order and the dispatch-slot priority derive from
+  // it, so "a lower member" is always a workgroup that has already started
+  // and the look-backs and the log read below never wait on one that has not
+  // been dispatched, whatever order the hardware dispatches in.
+  if (tid == 0) vbS = takeTicket(A().ticket, A().grid, A().skew);
+  uint32_t vb = 0;  // set after the first barrier
   // the lane's half (0: lanes 0-31, 1: lanes 32-63), recomputed at each use
   // by three VALU instructions: held live across the pipeline it spills, and
   // a reload's vmcnt wait drains the input loads in flight
@@ -278,14 +287,14 @@ __global__ __launch_bounds__(pc::kThreads) __attribute__((amdgpu_waves_per_eu(4,
   // work ahead of the last ones).
   auto teamX = [&](uint32_t& T, uint32_t& X) __attribute__((always_inline)) {
     const PCompArgs ka = A();
-    if (ka.xcdTeams) {  // w = xcd + 8 (group * team + x), team T = group * 8 + xcd
-      const uint32_t xcd = blockIdx.x & 7u, q = blockIdx.x >> 3;
+    if (ka.xcdTeams) {  // vb = xcd + 8 (group * team + x), team T = group * 8 + xcd
+      const uint32_t xcd = vb & 7u, q = vb >> 3;
       const uint32_t grp = q / ka.team;
       X = q - grp * ka.team;
       T = grp * 8 + xcd;
     } else {
-      T = blockIdx.x / ka.team;
-      X = blockIdx.x - T * ka.team;
+      T = vb / ka.team;
+      X = vb - T * ka.team;
     }
   };
   // item of element e (>= nb: none) for this member
@@ -727,7 +736,8 @@ __global__ __launch_bounds__(pc::kThreads) __attribute__((amdgpu_waves_per_eu(4,
   // stream run one after another, so nothing reads that counter now
   if (blockIdx.x == 0 && tid == 0)
     __hip_atomic_store(G(A().ctr) + ((A().epoch + 1) & 1u), 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __syncthreads();  // histogram zeroed
+  __syncthreads();  // histogram zeroed, ticket in
+  vb = readfirst(vbS);
   uint32_t round = 0;
   uint32_t iE = A().items, iL = itemOfElem(elemOfRound(0));
   if (iL >= A().items) return;
@@ -741,7 +751,7 @@ __global__ __launch_bounds__(pc::kThreads) __attribute__((amdgpu_waves_per_eu(4,
     // launch); rotating gives each slot each level in turn.  (The hand-off
     // window runs above all of them.)
     {
-      const uint32_t pr = (blockIdx.x / A().slotSpan + round) % 3u;
+      const uint32_t pr = (vb / A().slotSpan + round) % 3u;
       if (pr == 0) __builtin_amdgcn_s_setprio(0);
       else if (pr == 1) __builtin_amdgcn_s_setprio(1);
       else __builtin_amdgcn_s_setprio(2);

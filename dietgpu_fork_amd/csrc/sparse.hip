@@ -78,47 +78,18 @@ __device__ __forceinline__ void loadTile(gp<const W> x, uint32_t t0, uint32_t ti
   }
 }
 
-// s1: bitmap + tile count + tile-local compaction.  grid (tiles, batch); a
-// workgroup takes one 4096-word tile of one element into LDS, then each wave
-// takes 1024 consecutive words as 16 steps of 64 lanes: the ballot of nonzero
-// flags is the step's 64 bitmap bits (generate_bitmap :40-71) and its
-// nonzeros' ranks (v_mbcnt).  The nonzeros go, in order, to the tile's slice
-// of a staging area; the n-2 quirk (fill_comp_input :162-184) is one extra
-// staged slot: when x[n-2] == 0, a 0 precedes x[n-1]'s slot.  (A persistent
-// grid streaming several tiles per workgroup measured slower: its live state
-// halves the occupancy, and a wave's wait for its next tile's loads also
-// drains its stores.)
-//
-// kHist: the staged words are also counted into the dense codec's symbol
-// histogram(s) (the compacted list's symbols, the n-2 slot included) and
-// added into row tile % nRows of [segments][nb][nRows][256] (PartialHist,
-// zeroed by the host), so the dense codec skips its histogram pass over the
-// list.
-template <int FT, bool kVec, bool kHist>
-__global__ __launch_bounds__(kThreads) void k_sparseCount(BatchDesc in, const uint64_t* outPtrs,
-                                                          uint32_t batchOffset, uint32_t numInBatch,
-                                                          uint32_t tilesPerElem,
-                                                          uint32_t* __restrict__ tileCounts,
-                                                          WordOf<FT>* __restrict__ staging,
-                                                          uint32_t* __restrict__ histRows, uint32_t nRows) {
-  using W = WordOf<FT>;
+// One tile of k_sparseCount (t0 < n).
+template <int FT, bool kVec, bool kHist, typename W, typename HS>
+__device__ __forceinline__ void sparseCountTile(const BatchDesc& in, gp<uint8_t> o, uint32_t b, uint32_t n,
+                                                uint32_t tile, uint32_t numInBatch, uint32_t tilesPerElem,
+                                                uint32_t* __restrict__ tileCounts, W* __restrict__ staging,
+                                                uint32_t* __restrict__ histRows, uint32_t nRows, W* buf, HS& hs,
+                                                uint32_t* waveCnt) {
   constexpr int kSegs = FloatTraits<FT>::kSegs;
   constexpr uint32_t kSteps = kTileWords / kWaves / 64;
   constexpr uint32_t kCols = 4;  // LDS counter columns per bin (lane & 3)
-  __shared__ __attribute__((aligned(16))) W buf[kTileWords];
-  __shared__ __attribute__((aligned(16))) uint32_t hs[kHist ? kSegs : 1][kHist ? kNumSymbols * kCols : 4];
-  __shared__ uint32_t waveCnt[kWaves];
-  const uint32_t b = batchOffset + blockIdx.y;
-  const uint32_t n = in.size(b);
-  const uint32_t tile = blockIdx.x;
   const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  gp<uint8_t> o = (gp<uint8_t>)outPtrs[b];
-  if (tile == 0 && tid == 0) st16(o, make_uint4(n, 0, 0, 0));
   const uint32_t t0 = tile * kTileWords;
-  if (t0 >= n) {
-    if (tid == 0) tileCounts[uint64_t(b) * tilesPerElem + tile] = 0;
-    return;
-  }
   if constexpr (kHist) {
     for (int sg = 0; sg < kSegs; ++sg)
       for (uint32_t i = tid; i < kNumSymbols * kCols / 4; i += kThreads)
@@ -198,6 +169,66 @@ __global__ __launch_bounds__(kThreads) void k_sparseCount(BatchDesc in, const ui
   }
 }
 
+// s1: bitmap + tile count + tile-local compaction.  grid (tiles, batch); a
+// workgroup takes one 4096-word tile of one element into LDS, then each wave
+// takes 1024 consecutive words as 16 steps of 64 lanes: the ballot of nonzero
+// flags is the step's 64 bitmap bits (generate_bitmap :40-71) and its
+// nonzeros' ranks (v_mbcnt).  The nonzeros go, in order, to the tile's slice
+// of a staging area; the n-2 quirk (fill_comp_input :162-184) is one extra
+// staged slot: when x[n-2] == 0, a 0 precedes x[n-1]'s slot.  (A persistent
+// grid streaming several tiles per workgroup measured slower: its live state
+// halves the occupancy, and a wave's wait for its next tile's loads also
+// drains its stores.)
+//
+// kHist: the staged words are also counted into the dense codec's symbol
+// histogram(s) (the compacted list's symbols, the n-2 slot included) and
+// added into row tile % nRows of [segments][nb][nRows][256] (PartialHist,
+// zeroed by the host), so the dense codec skips its histogram pass over the
+// list; and the element's last tile to arrive (NormArgs::arrive, the counter
+// hand-off of k_hist) normalises the rows into the encode table and pdf, so
+// the dense codec skips its normalisation launch too (c4 1 x 15M fp32).
+template <int FT, bool kVec, bool kHist>
+__global__ __launch_bounds__(kThreads) void k_sparseCount(BatchDesc in, BatchDesc outD,
+                                                          uint32_t batchOffset, uint32_t numInBatch,
+                                                          uint32_t tilesPerElem,
+                                                          uint32_t* __restrict__ tileCounts,
+                                                          WordOf<FT>* __restrict__ staging,
+                                                          uint32_t* __restrict__ histRows, uint32_t nRows,
+                                                          NormArgs na) {
+  using W = WordOf<FT>;
+  constexpr int kSegs = FloatTraits<FT>::kSegs;
+  constexpr uint32_t kCols = 4;  // LDS counter columns per bin (lane & 3)
+  __shared__ __attribute__((aligned(16))) W buf[kTileWords];
+  __shared__ __attribute__((aligned(16))) uint32_t hs[kHist ? kSegs : 1][kHist ? kNumSymbols * kCols : 4];
+  __shared__ uint32_t waveCnt[kWaves];
+  __shared__ uint32_t arriveS;
+  static_assert(sizeof(buf) >= kNumSymbols * 4 + kThreads * 16 + 64, "normalisation scratch in buf");
+  const uint32_t b = batchOffset + blockIdx.y;
+  const uint32_t n = in.size(b);
+  const uint32_t tile = blockIdx.x;
+  const uint32_t tid = threadIdx.x;
+  gp<uint8_t> o = startOf(outD, b);
+  if (tile == 0 && tid == 0) st16(o, make_uint4(n, 0, 0, 0));
+  const uint32_t t0 = tile * kTileWords;
+  if (t0 >= n) {
+    if (tid == 0) tileCounts[uint64_t(b) * tilesPerElem + tile] = 0;
+  } else {
+    sparseCountTile<FT, kVec, kHist>(in, o, b, n, tile, numInBatch, tilesPerElem, tileCounts, staging, histRows,
+                                     nRows, buf, hs, waveCnt);
+  }
+  if constexpr (kHist) {
+    // every tile arrives (empty ones too); the last normalises the element
+    if (na.arrive && lastArrival(na.arrive + b, tilesPerElem, &arriveS)) {
+      uint32_t* scratch = reinterpret_cast<uint32_t*>(&buf[0]);
+      for (int sg = 0; sg < kSegs; ++sg) {
+        normalizeElement(na, numInBatch, b, sg, scratch, scratch + kNumSymbols,
+                         reinterpret_cast<u32x4*>(scratch + kNumSymbols + 16));
+        __syncthreads();
+      }
+    }
+  }
+}
+
 // Sum of counts[0, k) by the whole workgroup: 16 loads in flight per thread
 // (4,096 counts per memory round trip; an element of 16 M words has 4,096
 // tiles).  Every workgroup of an element sums its own prefix of the tile
@@ -235,7 +266,11 @@ __global__ __launch_bounds__(kThreads) void k_sparseGather(BatchDesc in, uint32_
   const uint32_t b = batchOffset + blockIdx.y;
   const uint32_t n = in.size(b);
   const uint32_t tile = blockIdx.x;
-  if (tile * kTileWords >= n) return;
+  if (tile * kTileWords >= n) {
+    // an empty element has no last tile: its (empty) list length is written here
+    if (n == 0 && tile == 0 && threadIdx.x == 0) listLen[b] = 0;
+    return;
+  }
   const uint64_t row = uint64_t(b) * tilesPerElem + tile;
   const uint32_t cnt = tileCounts[row];
   const uint32_t off = tilePrefix(G(tileCounts) + uint64_t(b) * tilesPerElem, tile, red);
@@ -350,10 +385,15 @@ __global__ __launch_bounds__(kThreads) void k_sparseExpand(BatchDesc in, BatchDe
   }
 }
 
+// in: the sparse inputs (sizes = N); outD: the sparse archives; denseOut:
+// where each dense archive starts; sparseN: a device array holding each
+// element's N (the dense archive's size writer adds the sparse header and
+// bitmap to outSize, EncTail::sparseN).
 template <int FT>
 void sparseCompressT(StackDeviceMemory& res, const FloatCompressConfig& config, uint32_t nb,
-                     const BatchDesc& in, uint32_t maxN, const uint64_t* outPtrs_dev,
-                     const BatchDesc& denseOut, uint32_t* outSize_dev, hipStream_t s, bool inAligned16) {
+                     const BatchDesc& in, uint32_t maxN, const BatchDesc& outD,
+                     const BatchDesc& denseOut, const uint32_t* sparseN, uint32_t* outSize_dev, hipStream_t s,
+                     bool inAligned16) {
   const uint32_t tiles = std::max(1u, divUp(maxN, kTileWords));
   auto tileCounts = res.alloc<uint32_t>(s, size_t(nb) * tiles);
   auto listLen = res.alloc<uint32_t>(s, nb);
@@ -367,40 +407,59 @@ void sparseCompressT(StackDeviceMemory& res, const FloatCompressConfig& config, 
   lists.sizes = listLen.data();
   // the list's symbol histogram, counted here for a single element when the
   // three-kernel dense path follows (the single-pass compressor counts as it
-  // loads).  It saves the dense path's histogram launches (c4 1 x 15M fp32:
-  // compress 85 -> 75 us) but lengthens every tile's workgroup, so with
-  // more elements the separate k_hist over the compacted lists is faster
-  // (5 x 15M: 155 us against 170).
+  // loads), and normalised by the element's last tile: the dense codec then
+  // runs k_encode alone (c4 1 x 15M fp32: compress 85 -> 75 us for the
+  // histogram; the normalisation launch ~7 us more).  It lengthens every
+  // tile's workgroup, so with more elements the separate k_hist over the
+  // compacted lists is faster (5 x 15M: 155 us against 170).
   const bool countHist = nb == 1 && (FT == 4 || !persistentFits(maxN));
   constexpr int kSegs = FloatTraits<FT>::kSegs;
   // histogram rows: up to 64 per element, accumulated with atomics
   const uint32_t G = tiles;
   const uint32_t R = std::min(tiles, kReduceRows);
   auto hist = res.alloc<uint32_t>(s, countHist ? size_t(kSegs) * nb * R * kNumSymbols : 1);
+  auto table = res.alloc<uint4>(s, countHist ? size_t(kSegs) * nb * kNumSymbols : 1);
+  auto pdf = res.alloc<uint16_t>(s, countHist ? size_t(kSegs) * nb * kNumSymbols : 1);
   if (countHist) HIP_CHECK(hipMemsetAsync(hist.data(), 0, size_t(kSegs) * nb * R * kNumSymbols * 4, s));
-  for (uint32_t y0 = 0; y0 < nb; y0 += kMaxGridY) {
-    const uint32_t ny = std::min(kMaxGridY, nb - y0);
-    prof::Scope p("sparse", s);
-    auto launch = [&](auto vecTag, auto histTag) {
-      k_sparseCount<FT, decltype(vecTag)::value, decltype(histTag)::value><<<dim3(G, ny), kThreads, 0, s>>>(
-          in, outPtrs_dev, y0, nb, tiles, tileCounts.data(), staging.data(), hist.data(), R);
-    };
-    if (inAligned16) {
-      if (countHist) launch(std::true_type{}, std::true_type{});
-      else launch(std::true_type{}, std::false_type{});
-    } else {
-      if (countHist) launch(std::false_type{}, std::true_type{});
-      else launch(std::false_type{}, std::false_type{});
+  {
+    // last-arrival counters of the normalising tile (self-resetting); the
+    // lease ends before the dense codec takes its own
+    const size_t regions[kSyncRegions] = {0, 0, 0, 0, size_t(nb) * 4};
+    SyncLease lease(res, s, regions);
+    NormArgs na{};
+    na.in = in;
+    na.hist = hist.data();
+    na.rows = R;
+    na.pb = config.ansConfig.probBits;
+    na.table = table.data();
+    na.pdf = pdf.data();
+    na.arrive = countHist ? static_cast<uint32_t*>(lease.base[kSyncArrive]) : nullptr;
+    na.totalFromHist = true;
+    for (uint32_t y0 = 0; y0 < nb; y0 += kMaxGridY) {
+      const uint32_t ny = std::min(kMaxGridY, nb - y0);
+      prof::Scope p("sparse", s);
+      auto launch = [&](auto vecTag, auto histTag) {
+        k_sparseCount<FT, decltype(vecTag)::value, decltype(histTag)::value><<<dim3(G, ny), kThreads, 0, s>>>(
+            in, outD, y0, nb, tiles, tileCounts.data(), staging.data(), hist.data(), R, na);
+      };
+      if (inAligned16) {
+        if (countHist) launch(std::true_type{}, std::true_type{});
+        else launch(std::true_type{}, std::false_type{});
+      } else {
+        if (countHist) launch(std::false_type{}, std::true_type{});
+        else launch(std::false_type{}, std::false_type{});
+      }
+      HIP_LAUNCH_CHECK();
+      k_sparseGather<FT><<<dim3(tiles, ny), kThreads, 0, s>>>(in, y0, tiles, tileCounts.data(), listLen.data(),
+                                                               staging.data(), lists);
+      HIP_LAUNCH_CHECK();
     }
-    HIP_LAUNCH_CHECK();
-    k_sparseGather<FT><<<dim3(tiles, ny), kThreads, 0, s>>>(in, y0, tiles, tileCounts.data(), listLen.data(),
-                                                             staging.data(), lists);
-    HIP_LAUNCH_CHECK();
   }
-  const PartialHist pre{hist.data(), R};
-  // the dense archive's writer adds the sparse header + bitmap to outSize
+  PartialHist pre{hist.data(), R};
+  pre.table = table.data();
+  pre.pdf = pdf.data();
   floatCompressDescs(res, config, nb, lists, maxN, denseOut, outSize_dev, s, nullptr, true,
-                     countHist ? &pre : nullptr, in.sizes);
+                     countHist ? &pre : nullptr, sparseN);
 }
 
 template <int FT>
@@ -492,27 +551,42 @@ void floatCompressSparse(StackDeviceMemory& res, const FloatCompressConfig& conf
     dp[i] = op[i] + 16 + roundUp((sz[i] + 7) / 8, 16);
     maxN = std::max(maxN, sz[i]);
   }
-  std::vector<uint64_t> ptrs(ip);
-  ptrs.insert(ptrs.end(), op.begin(), op.end());
-  ptrs.insert(ptrs.end(), dp.begin(), dp.end());
-  auto tbl = res.alloc<uint8_t>(stream, ptrs.size() * 8 + sz.size() * 4);
-  std::vector<uint8_t> host(ptrs.size() * 8 + sz.size() * 4);
-  std::memcpy(host.data(), ptrs.data(), ptrs.size() * 8);
-  std::memcpy(host.data() + ptrs.size() * 8, sz.data(), sz.size() * 4);
-  StackDeviceMemory::copyToDevice(tbl.data(), host.data(), host.size(), stream);
-  const uint64_t* ipD = reinterpret_cast<const uint64_t*>(tbl.data());
-  const uint64_t* opD = ipD + numInBatch;
-  const uint64_t* dpD = opD + numInBatch;
-  const uint32_t* szD = reinterpret_cast<const uint32_t*>(dpD + numInBatch);
-  auto inD = BatchDesc::pointers(ipD, szD);
-  auto denseOut = BatchDesc::pointers(dpD, nullptr);
   bool aligned = true;
   for (uint32_t i = 0; i < numInBatch; ++i) aligned = aligned && ip[i] % 16 == 0;
+  GpuMemoryReservation<uint8_t> tbl;
+  BatchDesc inD, outD, denseOut;
+  const uint32_t* sparseN;
+  if (numInBatch == 1) {
+    // one element (the reference's SparseFloatBenchmark shape): stride
+    // descriptors, no table upload; the dense archive's size writer reads N
+    // from the sparse header k_sparseCount writes first (word 0 of the archive)
+    inD = BatchDesc::strided(in[0], 0, sz[0]);
+    outD = BatchDesc::strided(out[0], 0, 0);
+    denseOut = BatchDesc::strided(reinterpret_cast<void*>(dp[0]), 0, 0);
+    sparseN = reinterpret_cast<const uint32_t*>(out[0]);
+  } else {
+    std::vector<uint64_t> ptrs(ip);
+    ptrs.insert(ptrs.end(), op.begin(), op.end());
+    ptrs.insert(ptrs.end(), dp.begin(), dp.end());
+    tbl = res.alloc<uint8_t>(stream, ptrs.size() * 8 + sz.size() * 4);
+    std::vector<uint8_t> host(ptrs.size() * 8 + sz.size() * 4);
+    std::memcpy(host.data(), ptrs.data(), ptrs.size() * 8);
+    std::memcpy(host.data() + ptrs.size() * 8, sz.data(), sz.size() * 4);
+    StackDeviceMemory::copyToDevice(tbl.data(), host.data(), host.size(), stream);
+    const uint64_t* ipD = reinterpret_cast<const uint64_t*>(tbl.data());
+    const uint64_t* opD = ipD + numInBatch;
+    const uint64_t* dpD = opD + numInBatch;
+    const uint32_t* szD = reinterpret_cast<const uint32_t*>(dpD + numInBatch);
+    inD = BatchDesc::pointers(ipD, szD);
+    outD = BatchDesc::pointers(opD, nullptr);
+    denseOut = BatchDesc::pointers(dpD, nullptr);
+    sparseN = szD;
+  }
   switch (ft) {
-    case 1: sparseCompressT<1>(res, config, numInBatch, inD, maxN, opD, denseOut, outSize_dev, stream, aligned); break;
-    case 2: sparseCompressT<2>(res, config, numInBatch, inD, maxN, opD, denseOut, outSize_dev, stream, aligned); break;
-    case 3: sparseCompressT<3>(res, config, numInBatch, inD, maxN, opD, denseOut, outSize_dev, stream, aligned); break;
-    default: sparseCompressT<4>(res, config, numInBatch, inD, maxN, opD, denseOut, outSize_dev, stream, aligned); break;
+    case 1: sparseCompressT<1>(res, config, numInBatch, inD, maxN, outD, denseOut, sparseN, outSize_dev, stream, aligned); break;
+    case 2: sparseCompressT<2>(res, config, numInBatch, inD, maxN, outD, denseOut, sparseN, outSize_dev, stream, aligned); break;
+    case 3: sparseCompressT<3>(res, config, numInBatch, inD, maxN, outD, denseOut, sparseN, outSize_dev, stream, aligned); break;
+    default: sparseCompressT<4>(res, config, numInBatch, inD, maxN, outD, denseOut, sparseN, outSize_dev, stream, aligned); break;
   }
 }
 
@@ -534,18 +608,25 @@ FloatDecompressStatus floatDecompressSparse(StackDeviceMemory& res,
     cap[i] = outCapacity[i];
     maxCap = std::max(maxCap, cap[i]);
   }
-  auto tbl = res.alloc<uint8_t>(stream, ptrs.size() * 8 + cap.size() * 4);
-  std::vector<uint8_t> host(ptrs.size() * 8 + cap.size() * 4);
-  std::memcpy(host.data(), ptrs.data(), ptrs.size() * 8);
-  std::memcpy(host.data() + ptrs.size() * 8, cap.data(), cap.size() * 4);
-  StackDeviceMemory::copyToDevice(tbl.data(), host.data(), host.size(), stream);
-  const uint64_t* ipD = reinterpret_cast<const uint64_t*>(tbl.data());
-  const uint64_t* opD = ipD + numInBatch;
-  const uint32_t* capD = reinterpret_cast<const uint32_t*>(opD + numInBatch);
-  auto inD = BatchDesc::pointers(ipD, nullptr);
-  auto outD = BatchDesc::pointers(opD, capD);
   bool aligned = true;
   for (uint32_t i = 0; i < numInBatch; ++i) aligned = aligned && ptrs[numInBatch + i] % 16 == 0;
+  GpuMemoryReservation<uint8_t> tbl;
+  BatchDesc inD, outD;
+  if (numInBatch == 1) {  // stride descriptors, no table upload
+    inD = BatchDesc::strided(in[0], 0, 0);
+    outD = BatchDesc::strided(out[0], 0, cap[0]);
+  } else {
+    tbl = res.alloc<uint8_t>(stream, ptrs.size() * 8 + cap.size() * 4);
+    std::vector<uint8_t> host(ptrs.size() * 8 + cap.size() * 4);
+    std::memcpy(host.data(), ptrs.data(), ptrs.size() * 8);
+    std::memcpy(host.data() + ptrs.size() * 8, cap.data(), cap.size() * 4);
+    StackDeviceMemory::copyToDevice(tbl.data(), host.data(), host.size(), stream);
+    const uint64_t* ipD = reinterpret_cast<const uint64_t*>(tbl.data());
+    const uint64_t* opD = ipD + numInBatch;
+    const uint32_t* capD = reinterpret_cast<const uint32_t*>(opD + numInBatch);
+    inD = BatchDesc::pointers(ipD, nullptr);
+    outD = BatchDesc::pointers(opD, capD);
+  }
   switch (ft) {
     case 1: return sparseDecompressT<1>(res, config, numInBatch, inD, outD, maxCap, outSuccess_dev, outSize_dev, stream, aligned);
     case 2: return sparseDecompressT<2>(res, config, numInBatch, inD, outD, maxCap, outSuccess_dev, outSize_dev, stream, aligned);

@@ -1,6 +1,7 @@
 // Per-(device, stream) flag arenas for k_compress (see sync_arena.h).
 #include "sync_arena.h"
 
+#include <algorithm>
 #include <atomic>
 #include <functional>
 #include <map>
@@ -19,6 +20,13 @@ struct Arena {
   void* ptr[kSyncRegions] = {};
   size_t bytes[kSyncRegions] = {};
   uint32_t epoch = 0;
+  // k_pcompress's two dequeue counters (kSyncCounters, u64 each): bit k set
+  // while counter k may hold an earlier call's count.  A k_pcompress call at
+  // epoch e uses counter e & 1 and zeroes counter (e + 1) & 1 for the next
+  // call; a call in between that does not run k_pcompress (the three-kernel
+  // path) still takes an epoch, so the counter a later k_pcompress call uses
+  // can be the dirty one: it is then zeroed here, stream-ordered.
+  uint32_t ctrDirty = 0;
 };
 
 using Key = std::tuple<int, hipStream_t, size_t>;
@@ -30,14 +38,21 @@ std::map<Key, std::unique_ptr<Arena>>& arenas() {
 
 std::atomic<uint32_t> gSpinCap{1u << 24};
 std::atomic<uint32_t> gBarrierBudget{20000};
+std::atomic<uint32_t> gDispatchSkew{0};
 }  // namespace
 
 void setSpinCap(uint32_t polls) { gSpinCap.store(polls); }
 uint32_t spinCap() { return gSpinCap.load(); }
 void setBarrierBudget(uint32_t ticks) { gBarrierBudget.store(ticks); }
 uint32_t barrierBudgetTicks() { return gBarrierBudget.load(); }
+void setDispatchSkew(uint32_t ticks) { gDispatchSkew.store(ticks); }
+uint32_t dispatchSkew() { return gDispatchSkew.load(); }
 
-SyncLease::SyncLease(StackDeviceMemory& res, hipStream_t stream, const size_t (&bytes)[kSyncRegions]) {
+SyncLease::SyncLease(StackDeviceMemory& res, hipStream_t stream, const size_t (&bytesIn)[kSyncRegions],
+                     bool dequeue) {
+  size_t bytes[kSyncRegions];
+  for (int k = 0; k < kSyncRegions; ++k) bytes[k] = bytesIn[k];
+  bytes[kSyncCounters] = std::max(bytes[kSyncCounters], kSyncCounterBytes);
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
   HIP_CHECK(hipStreamIsCapturing(stream, &cs));
   if (cs != hipStreamCaptureStatusNone) {
@@ -80,12 +95,20 @@ SyncLease::SyncLease(StackDeviceMemory& res, hipStream_t stream, const size_t (&
       HIP_CHECK(hipMalloc(&a->ptr[k], want));
       HIP_CHECK(hipMemsetAsync(a->ptr[k], 0, want, stream));
       a->bytes[k] = want;
+      if (k == kSyncCounters) a->ctrDirty = 0;
     }
   }
   a->epoch = (a->epoch + 1) & kEpochMask;
   if (a->epoch == 0) {  // wrapped: words of every older epoch must go
     for (int k = 0; k < kSyncRegions; ++k) HIP_CHECK(hipMemsetAsync(a->ptr[k], 0, a->bytes[k], stream));
     a->epoch = 1;
+    a->ctrDirty = 0;
+  }
+  if (dequeue) {  // a k_pcompress call: its counter must start at zero
+    const uint32_t mine = a->epoch & 1u;
+    if (a->ctrDirty & (1u << mine))
+      HIP_CHECK(hipMemsetAsync(static_cast<uint64_t*>(a->ptr[kSyncCounters]) + mine, 0, sizeof(uint64_t), stream));
+    a->ctrDirty = 1u << mine;  // the kernel zeroes the other one
   }
   for (int k = 0; k < kSyncRegions; ++k) base[k] = a->ptr[k];
   epoch = a->epoch;

@@ -40,12 +40,22 @@ constexpr uint32_t kEpochMask = 0xffffu;
 // encode.h): untagged, they wrap back to zero at every element's last
 // arrival, so they are zero between calls.
 enum SyncRegion : int { kSyncCounters = 0, kSyncFlags, kSyncPartials, kSyncLog, kSyncArrive, kSyncRegions };
+// kSyncCounters layout: k_pcompress's two u64 dequeue counters, then the u32
+// workgroup-ticket counter (takeTicket, device.h; self-resetting).
+constexpr size_t kSyncTicketOffset = 16;
+constexpr size_t kSyncCounterBytes = 32;
 
 class SyncLease {
  public:
   // Per region, >= `bytes[k]` zero-at-creation bytes for the current device
   // and `stream`, and this call's epoch (1 .. kEpochMask).
-  SyncLease(StackDeviceMemory& res, hipStream_t stream, const size_t (&bytes)[kSyncRegions]);
+  // dequeue: the call runs k_pcompress, whose dequeue counter (epoch & 1)
+  // must start at zero (see Arena::ctrDirty).
+  SyncLease(StackDeviceMemory& res, hipStream_t stream, const size_t (&bytes)[kSyncRegions], bool dequeue = false);
+
+  uint32_t* ticket() const {
+    return reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(base[kSyncCounters]) + kSyncTicketOffset);
+  }
   SyncLease(const SyncLease&) = delete;
   SyncLease& operator=(const SyncLease&) = delete;
 
@@ -75,5 +85,11 @@ uint32_t spinCap();
 // every team wait fall back at once: test hook for the slow path.
 void setBarrierBudget(uint32_t ticks);
 uint32_t barrierBudgetTicks();
+
+// Test hook: workgroups of the compressors wait (63 - g % 64) * ticks before
+// taking their start ticket (takeTicket, device.h), emulating out-of-order
+// dispatch.  0 (default) is off.
+void setDispatchSkew(uint32_t ticks);
+uint32_t dispatchSkew();
 
 }  // namespace dietgpu

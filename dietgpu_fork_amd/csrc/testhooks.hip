@@ -1,11 +1,16 @@
 // Test hooks (not part of the reference API): a bounded-duration kernel that
 // holds compute units, so tests can run the compressor while another kernel
-// occupies part of the chip (pcompress.h, "Forward progress").
+// occupies part of the chip (pcompress.h, "Forward progress"); and the byte
+// histogram of the three-kernel compressor's first pass exposed on its own,
+// as the reference's ANSStatisticsTest.cu:44-95 exercises ansHistogramBatch.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 
 #include "common.h"
+#include "dietgpu/StackDeviceMemory.h"
+#include "encode.h"
 
 namespace dietgpu {
 
@@ -25,7 +30,36 @@ __global__ __launch_bounds__(256) void k_occupy(uint64_t ticks, uint32_t* sink) 
   }
   if (acc == 0x9e3779b9u) sink[0] = acc;  // never: keeps the loop
 }
+
+// Sum of an element's per-chunk partial histograms (k_hist rows): grid nb.
+__global__ __launch_bounds__(kThreads) void k_sumChunkRows(const uint32_t* part, uint32_t chunks,
+                                                          uint32_t* out) {
+  __shared__ u32x4 red4[kThreads];
+  const uint32_t b = blockIdx.x;
+  const uint32_t v = sumRows256<false>(G(part) + uint64_t(b) * chunks * kNumSymbols, chunks, red4);
+  G(out)[uint64_t(b) * kNumSymbols + threadIdx.x] = v;
+}
 }  // namespace
+
+// hist[b][256] = byte histogram of element b of a stride batch (elements of
+// `size` bytes, `stride` bytes apart): k_hist<0> (the compressor's own
+// histogram kernel, chunked exactly as encodeBatchDevice chunks it) and a row
+// sum.  ansHistogramBatch (ans/GpuANSStatistics.cuh:113-143).
+void testHistogram(StackDeviceMemory& res, hipStream_t s, uint32_t nb, const void* in_dev, uint32_t size,
+                   uint32_t stride, uint32_t* hist_dev) {
+  if (nb == 0) return;
+  DG_CHECK(nb <= 65535, "at most 65535 elements");
+  const auto in = BatchDesc::strided(in_dev, stride, size);
+  uint32_t chunk = 64 * 1024;
+  while (divUp(size, chunk) > 4096) chunk *= 2;
+  const uint32_t chunks = std::max(1u, divUp(size, chunk));
+  auto part = res.alloc<uint32_t>(s, size_t(nb) * chunks * kNumSymbols);
+  NormArgs na{};
+  k_hist<0, false><<<dim3(chunks, nb), kThreads, 0, s>>>(in, 0, nb, chunk, chunks, part.data(), nullptr, na);
+  HIP_LAUNCH_CHECK();
+  k_sumChunkRows<<<nb, kThreads, 0, s>>>(part.data(), chunks, hist_dev);
+  HIP_LAUNCH_CHECK();
+}
 
 void testOccupy(hipStream_t s, uint32_t micros, uint32_t workgroups, uint32_t ldsBytes) {
   DG_CHECK(ldsBytes >= 1024 && ldsBytes <= 160 * 1024, "ldsBytes out of range");

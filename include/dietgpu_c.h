@@ -191,11 +191,23 @@ void dietgpu_set_spin_cap(uint32_t polls);
  * fallback keeps the compressor live when other kernels hold CUs; 0 forces
  * it for every team wait (archives are unchanged). */
 void dietgpu_set_barrier_budget(uint32_t ticks);
+/* Test hook: every compressor workgroup (k_pcompress, and k_encode on the
+ * fused three-kernel path) waits (63 - g % 64) * ticks (100 MHz) before it
+ * takes its start ticket, so tickets go out in about reverse launch order:
+ * out-of-order dispatch, emulated.  Archives are unchanged; 0 = off. */
+void dietgpu_set_dispatch_skew(uint32_t ticks);
 /* Test hook: enqueue on `stream` a kernel of `workgroups` 256-thread
  * workgroups that each hold `lds_bytes` of LDS for `micros` microseconds
  * (<= 1 s) and exit: compute units held by another kernel while the
  * compressor runs. */
 int dietgpu_test_occupy(void* stream, uint32_t micros, uint32_t workgroups, uint32_t lds_bytes);
+/* Test hook: hist_dev[b * 256 + s] = count of byte value s in element b of a
+ * stride batch (nb <= 65535 elements of `size` bytes, `stride` bytes apart),
+ * computed by the compressor's own histogram kernel.  Replaces the
+ * reference's ansHistogramBatch as its ANSStatisticsTest.cu:44-95 calls it
+ * (ans/GpuANSStatistics.cuh:113-143). */
+int dietgpu_test_histogram(dietgpu_stack* res, uint32_t nb, const void* in_dev, uint32_t size,
+                           uint32_t stride, uint32_t* hist_dev, void* stream);
 
 #ifdef __cplusplus
 }

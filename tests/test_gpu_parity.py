@@ -195,7 +195,7 @@ def test_float_stride_batch(C, ws, ft):
     np.testing.assert_array_equal(dec.cpu().numpy().view(NP_WORD[ft]), w)
 
 
-SPARSE_SIZES = [1, 2, 3, 17, 4096, 4097, 50001]
+SPARSE_SIZES = [0, 1, 2, 3, 17, 4096, 4097, 50001]
 
 
 @pytest.mark.parametrize("ft", [1, 2, 3, 4])
@@ -205,10 +205,10 @@ def test_sparse_parity(C, ws, ft):
         w = sparsify(float_words(ft, n, seed=40 + i), 0.9, seed=50 + i)
         words.append(w)
     # force both n-2 quirk branches
-    words[3][-2] = 0
-    words[4][-2] = 7
-    words[5][-2] = 0
-    words[5][-1] = 0
+    words[4][-2] = 0
+    words[5][-2] = 7
+    words[6][-2] = 0
+    words[6][-1] = 0
     ts = [to_dev_words(w, ft) for w in words]
     out, sizes = C.sparse_compress(ts, ft=ft, ws=ws)
     host = out.cpu().numpy()

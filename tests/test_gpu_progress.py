@@ -104,3 +104,37 @@ def test_compress_beside_occupying_kernel(C, ws):
     y, ok, _ = C.float_decompress_stride(out, 524288, torch.bfloat16, ws=ws)
     assert bool((ok == 1).all())
     assert torch.equal(y.view(torch.int16), x.view(torch.int16))
+
+
+@pytest.mark.parametrize("shape", ["c2", "c3"])
+def test_out_of_order_dispatch(C, ws, shape):
+    """Workgroups take their start tickets in about REVERSE launch order
+    (test hook: each waits (63 - g % 64) x 1 us first), emulating a dispatcher
+    that starts later workgroups first.  The look-backs (k_pcompress's team
+    look-back and log read; k_encode's fused look-back on the c3 path) order
+    workgroups by ticket, so they still only wait on started workgroups:
+    archives oracle-identical, nothing abandoned."""
+    C.device_error_count(reset=True)
+    try:
+        C.set_dispatch_skew(100)
+        if shape == "c2":  # single pass, 2 rounds of dequeued elements
+            nb = 320
+            words = [float_words(2, 524288, seed=300 + i) for i in range(nb)]
+            x = torch.from_numpy(np.stack(words).view(np.int16)).to(DEV).view(torch.bfloat16)
+            out, sizes = C.float_compress_stride(x, prob_bits=10, ws=ws)
+            refs = [O.float_compress(w, 2) for w in words]
+        else:  # 4 MiB byte elements: three kernels, 64 encode workgroups each
+            nb = 24
+            rng = np.random.default_rng(31)
+            data = rng.integers(0, 16, size=(nb, 4 * MIB), dtype=np.uint8)
+            out, sizes = C.ans_encode_stride(torch.from_numpy(data).to(DEV), ws=ws)
+            refs = [O.ans_encode(data[i]) for i in range(nb)]
+        torch.cuda.synchronize()
+    finally:
+        C.set_dispatch_skew(0)
+    assert C.device_error_count(reset=True) == 0
+    sizes = sizes.cpu().tolist()
+    host = out.cpu().numpy()
+    for i, ref in enumerate(refs):
+        assert sizes[i] == ref.size, (i, sizes[i], ref.size)
+        np.testing.assert_array_equal(host[i, : ref.size], ref, err_msg=f"element {i}")

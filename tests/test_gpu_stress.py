@@ -105,3 +105,46 @@ def test_float_batch_beyond_inline_tables(C, ws, nb):
     rng = np.random.default_rng(nb)
     xs = [_bf16_words(int(rng.integers(1, 6000)), seed=j) for j in range(nb)]
     _float_roundtrip(C, ws, xs)
+
+
+@pytest.mark.parametrize("middle", ["fp64", "unaligned"])
+def test_single_pass_after_three_kernel_call(C, ws, middle):
+    """Single-pass call of >= 3 rounds (elements past the static rounds come
+    from a dequeue counter), then a three-kernel call on the same stream (it
+    takes an epoch but never runs k_pcompress), then the single-pass call
+    again: the second single-pass call's counter must start at zero, or the
+    elements it would dequeue first are silently never encoded."""
+    nb, n = 3000, 4096  # one item per element: 1,024-member grid, 3 rounds
+    g = torch.Generator().manual_seed(11)
+    x = (torch.randn(nb, n, generator=g) * 3).to(torch.bfloat16)
+    xd = x.to(DEV).view(torch.int16)
+    words = x.view(torch.int16).numpy().view(np.uint16)
+    refs = [O.float_compress(words[i], 2) for i in range(nb)]
+
+    cols = C.max_float_compressed_size(2, n)
+
+    def single_pass():
+        # fresh sentinels: a dropped element must not find the last call's archive
+        out = torch.full([nb, cols], 0xAA, dtype=torch.uint8, device=DEV)
+        sizes = torch.full([nb], -1, dtype=torch.int32, device=DEV)
+        out, sizes = C.float_compress_stride(xd, ft=2, ws=ws, out=out, sizes=sizes)
+        sizes = sizes.cpu().tolist()
+        host = out.cpu().numpy()
+        for i in range(nb):
+            assert sizes[i] == refs[i].size, (i, sizes[i], refs[i].size)
+            np.testing.assert_array_equal(host[i, : refs[i].size], refs[i], err_msg=f"element {i}")
+
+    single_pass()
+    if middle == "fp64":
+        w64 = np.random.default_rng(3).standard_normal(70000).view(np.uint64)
+        t64 = torch.from_numpy(w64.view(np.int64).copy()).to(DEV)
+        out, sizes = C.float_compress_pointer([t64], ft=4, ws=ws)
+        ref = O.float_compress(w64, 4)
+        np.testing.assert_array_equal(out[0, : int(sizes[0])].cpu().numpy(), ref)
+    else:
+        big = xd.reshape(-1)
+        out, sizes = C.float_compress_pointer([big[1:50001]], ft=2, ws=ws)
+        ref = O.float_compress(words.reshape(-1)[1:50001], 2)
+        np.testing.assert_array_equal(out[0, : int(sizes[0])].cpu().numpy(), ref)
+    single_pass()
+    assert C.device_error_count(reset=True) == 0

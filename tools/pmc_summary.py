@@ -59,8 +59,14 @@ def main(src, tag):
             d["frac_wait_inst_any"] = d.get("SQ_WAIT_INST_ANY", 0) / w
             d["frac_active_inst"] = d.get("SQ_ACTIVE_INST_ANY", 0) / w
         res[fam] = d
+    sys.path.insert(0, ROOT)
+    from bench import library_sha256
+
     json.dump({"source": "rocprofv3 --pmc (separate passes), tools/profile_gpu.sh",
                "hbm_formula": "(2*FETCH_SIZE + WRITE_SIZE) * 1024",
+               # the build the counters describe (bench.py takes traffic only
+               # from a summary of the library it runs)
+               "library_sha256": library_sha256(),
                "kernels": res}, open(os.path.join(outdir, f"{tag}_pmc.json"), "w"), indent=1)
     print(json.dumps(res, indent=1))
 
