@@ -314,12 +314,14 @@ def _bf16_rows(first, last, n, dev, chunk=512):
 def _decode_cold_warm(step_parts, dev, reps=8, flush_bytes=512 << 20):
     """Isolated decode times (torch events on the launch stream): `warm`
     right after a compress (archives partly in the MALL, as in the timed
-    step), `cold` after a compress and a flush_bytes fill that evicts them
-    (the decoder then reads its archives from HBM)."""
+    step), `cold` after a compress and a read of a flush_bytes buffer that
+    evicts them (the decoder then reads its archives from HBM).  The flush
+    only reads, so it leaves no dirty lines whose write-back would land in
+    the timed decode."""
     import torch
 
     compress, decompress = step_parts
-    scratch = torch.empty(flush_bytes, dtype=torch.uint8, device=dev)
+    scratch = torch.ones(flush_bytes // 4, dtype=torch.int32, device=dev)
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     res = {}
     for name, flush in (("warm", False), ("cold", True)):
@@ -327,7 +329,7 @@ def _decode_cold_warm(step_parts, dev, reps=8, flush_bytes=512 << 20):
         for i in range(reps + 1):
             compress()
             if flush:
-                scratch.fill_(i & 0xFF)
+                scratch.sum()
             a.record()
             decompress()
             b.record()
@@ -336,7 +338,7 @@ def _decode_cold_warm(step_parts, dev, reps=8, flush_bytes=512 << 20):
                 tot += a.elapsed_time(b)
         res[f"decode_{name}_ms"] = round(tot / reps, 5)
     del scratch
-    res["note"] = (f"decode timed alone after a compress; cold: a {flush_bytes >> 20} MiB fill between them "
+    res["note"] = (f"decode timed alone after a compress; cold: a {flush_bytes >> 20} MiB read between them "
                    "evicts the archives from the 256 MiB Infinity Cache")
     return res
 

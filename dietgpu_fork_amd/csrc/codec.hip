@@ -235,11 +235,13 @@ bool compressPersistent(StackDeviceMemory& res, int pb, bool useChecksum, uint32
   const size_t partBytes = size_t(items) * kNumSymbols * 4;
   const uint32_t teams = grid / team;
   const uint32_t maxR = 2 * divUp(nb, teams) + 2;
-  const size_t regions[kSyncRegions] = {16, size_t(items) * 8, partBytes + (kCk ? size_t(items) * 4 : 0),
-                                        size_t(teams) * maxR * 8, 0};
+  // (counters region: the dequeue counters, then one start-ticket counter
+  // per team)
+  const size_t regions[kSyncRegions] = {kSyncTicketOffset + size_t(teams) * 4, size_t(items) * 8,
+                                        partBytes + (kCk ? size_t(items) * 4 : 0), size_t(teams) * maxR * 8, 0};
   SyncLease lease(res, s, regions, /*dequeue=*/true);
   if (FT != 0 && useChecksum) {
-    HIP_CHECK(hipMemsetAsync(ck.data(), 0, sizeof(uint32_t) * nb, s));
+    zeroAsync(ck.data(), sizeof(uint32_t) * nb, s);
     // float checksum: the reference passes float-word counts as byte counts
     // (float/GpuFloatCompress.cuh:709)
     const uint32_t ckChunk = 1u << 20;
@@ -297,7 +299,6 @@ void encodeBatchDevice(StackDeviceMemory& res, int pb, bool useChecksum, uint32_
   const uint32_t MB = divUp(maxSize, kBlockSize);
   const bool userHist = FT == 0 && hist_dev != nullptr;
   const bool preHist = FT != 0 && pre != nullptr;  // partial rows counted by the caller
-  const bool preNorm = preHist && pre->table != nullptr;  // ... and normalised
   const uint32_t chunkWords = histChunkWords(nb, maxSize);
   const uint32_t chunks = preHist ? std::max(1u, pre->nRows) : std::max(1u, divUp(maxSize, chunkWords));
   const bool runHist = !preHist && (!userHist || useChecksum);
@@ -320,14 +321,14 @@ void encodeBatchDevice(StackDeviceMemory& res, int pb, bool useChecksum, uint32_
   const uint32_t* chunkRows = preHist ? pre->rows : partHist.data();
   // first-level sums when elements have many chunks (k_histReduce)
   const uint32_t groups = divUp(chunks, kReduceRows);
-  const bool reduce2 = (runHist || preHist) && !preNorm && chunks > kReduceRows;
+  const bool reduce2 = (runHist || preHist) && chunks > kReduceRows;
   auto groupHist = res.alloc<uint32_t>(s, reduce2 ? size_t(kSegs) * nb * groups * kNumSymbols : 1);
   auto groupCk = res.alloc<uint32_t>(s, reduce2 && rawCk ? size_t(nb) * groups : 1);
   auto ck = res.alloc<uint32_t>(s, nb);
-  auto tableMem = res.alloc<uint4>(s, preNorm ? 1 : size_t(kSegs) * nb * kNumSymbols);
-  auto pdfMem = res.alloc<uint16_t>(s, preNorm ? 1 : size_t(kSegs) * nb * kNumSymbols);
-  const uint4* table = preNorm ? pre->table : tableMem.data();
-  const uint16_t* pdf = preNorm ? pre->pdf : pdfMem.data();
+  auto tableMem = res.alloc<uint4>(s, size_t(kSegs) * nb * kNumSymbols);
+  auto pdfMem = res.alloc<uint16_t>(s, size_t(kSegs) * nb * kNumSymbols);
+  const uint4* table = tableMem.data();
+  const uint16_t* pdf = pdfMem.data();
   auto slots = res.alloc<uint8_t>(s, size_t(kSegs) * nb * std::max(MB, 1u) * kSlotBytes);
   auto cw = res.alloc<uint32_t>(s, kFused ? 1 : size_t(kSegs) * nb * std::max(MB, 1u));
   const uint32_t nW = std::max(1u, divUp(MB, EncCfg<FT>::kBlocksPerWG));
@@ -340,8 +341,8 @@ void encodeBatchDevice(StackDeviceMemory& res, int pb, bool useChecksum, uint32_
   const bool finalInReduce = reduce2;
   const bool finalInHist = !reduce2 && runHist && uint64_t(chunks) * nb <= 4096;
   // k_encode's look-back flags (fused formats: one per element and encode
-  // workgroup, epoch-tagged, never zeroed), the start-ticket counter and the
-  // last-arrival counters, in this stream's sync arena
+  // workgroup, epoch-tagged, never zeroed) and the last-arrival counters, in
+  // this stream's sync arena
   const size_t regions[kSyncRegions] = {0, kFused ? size_t(nb) * nW * 8 : 0, 0, 0, size_t(nb) * 4};
   SyncLease lease(res, s, regions);
   NormArgs na;
@@ -359,7 +360,7 @@ void encodeBatchDevice(StackDeviceMemory& res, int pb, bool useChecksum, uint32_
   naFinal.arrive = static_cast<uint32_t*>(lease.base[kSyncArrive]);
 
   if (FT != 0 && useChecksum) {
-    HIP_CHECK(hipMemsetAsync(ck.data(), 0, sizeof(uint32_t) * nb, s));
+    zeroAsync(ck.data(), sizeof(uint32_t) * nb, s);
   }
   for (uint32_t y0 = 0; y0 < nb; y0 += kMaxGridY) {
     const uint32_t ny = std::min(kMaxGridY, nb - y0);
@@ -392,7 +393,7 @@ void encodeBatchDevice(StackDeviceMemory& res, int pb, bool useChecksum, uint32_
                                           finalInReduce ? naFinal : na, kSegs);
       HIP_LAUNCH_CHECK();
     }
-    if (!finalInReduce && !finalInHist && !preNorm) {
+    if (!finalInReduce && !finalInHist) {
       prof::Scope p("normalize", s);
       dim3 g(ny, kSegs);
       k_normalize<<<g, kThreads, 0, s>>>(na, y0, nb);
@@ -405,7 +406,6 @@ void encodeBatchDevice(StackDeviceMemory& res, int pb, bool useChecksum, uint32_
                    kFused ? static_cast<uint64_t*>(lease.base[kSyncFlags]) : nullptr, nW, pb, useChecksum,
                    spinCap(), deviceErrorWord(), sparseN};
       tail.epoch = lease.epoch;
-      tail.ticket = kFused ? lease.ticket() : nullptr;
       tail.skew = dispatchSkew();
       k_encode<FT, 0><<<g, enc::kThreads, 0, s>>>(in, out, y0, nb, std::max(MB, 1u), table,
                                                slots.data(), cw.data(), tail);
@@ -485,7 +485,7 @@ std::vector<std::pair<int, std::string>> verifyChecksums(StackDeviceMemory& res,
   const BatchDesc archives = dd.map(archivesArg), decoded = dd.map(decodedArg);
   auto now = res.alloc<uint32_t>(s, nb);
   auto old = res.alloc<uint32_t>(s, nb);
-  HIP_CHECK(hipMemsetAsync(now.data(), 0, sizeof(uint32_t) * nb, s));
+  zeroAsync(now.data(), sizeof(uint32_t) * nb, s);
   const uint32_t ckChunk = 1u << 20;
   for (uint32_t y0 = 0; y0 < nb; y0 += kMaxGridY) {
     const uint32_t ny = std::min(kMaxGridY, nb - y0);

@@ -99,6 +99,13 @@ struct DietGpuError : public std::runtime_error {
 
 #define HIP_LAUNCH_CHECK() HIP_CHECK(hipGetLastError())
 
+// Zero `bytes` of device memory in stream order with a kernel (upload.hip).
+// Used instead of hipMemsetAsync everywhere: a memset captured into a
+// hipGraph was not re-run on every replay on this ROCm (256 B and 1 MiB
+// nodes kept their first replay's effect, tools/debug/memset_probe.py),
+// while a kernel node is.
+void zeroAsync(void* dst, size_t bytes, hipStream_t s);
+
 // ---------------------------------------------------------------------------
 // device helpers (gfx950 wave64)
 // ---------------------------------------------------------------------------

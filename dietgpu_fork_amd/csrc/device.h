@@ -235,15 +235,18 @@ __device__ __forceinline__ void stSc1(gp<uint32_t> p, uint32_t v) {
 // (63 - g % 64) * skew ticks of the 100 MHz clock, so tickets go out in about
 // reverse launch order within every 64 workgroups -- out-of-order dispatch,
 // emulated.  One lane.
-__device__ __forceinline__ uint32_t takeTicket(uint32_t* counter, uint32_t count, uint32_t skew) {
+__device__ __forceinline__ void skewDelay(uint32_t skew) {
 #if defined(__HIP_DEVICE_COMPILE__)
-  if (skew) {
-    const uint32_t g = blockIdx.y * gridDim.x + blockIdx.x;
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    const uint64_t d = uint64_t(63 - (g & 63)) * skew;
-    while (__builtin_amdgcn_s_memrealtime() - t0 < d) __builtin_amdgcn_s_sleep(8);
-  }
+  const uint32_t g = blockIdx.y * gridDim.x + blockIdx.x;
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  const uint64_t d = uint64_t(63 - (g & 63)) * skew;
+  while (__builtin_amdgcn_s_memrealtime() - t0 < d) __builtin_amdgcn_s_sleep(8);
+#else
+  (void)skew;
 #endif
+}
+__device__ __forceinline__ uint32_t takeTicket(uint32_t* counter, uint32_t count, uint32_t skew) {
+  if (skew) skewDelay(skew);
   return atomicInc(counter, count - 1);
 }
 

@@ -13,9 +13,12 @@
 // block pair per wave); the items of an element form its team.  The grid is
 // at most one generation of resident workgroups, a whole number of teams of
 // workgroups, and a workgroup team takes one element per round: member x of
-// team T works item x of the team's element.  Workgroups are numbered by
-// start ticket (vb, see below); member x of team T has a higher ticket than
-// members 0 .. x-1.  Elements of rounds 0 and 1 are static (r * teams + T); from
+// team T works item x of the team's element.  Team membership comes from
+// blockIdx and keeps each team on one XCD (workgroups w, w + 8, ... share one
+// under the observed round-robin placement), so the team's hand-offs stay in
+// one L2 (speed only, never correctness); the member index x is the order in
+// which the team's workgroups started (a per-team start ticket, below).
+// Elements of rounds 0 and 1 are static (r * teams + T); from
 // round 2 on, member 0 takes the team's element two rounds ahead with one
 // returning add on a per-call counter and logs it (epoch-tagged) for the
 // other members, so teams that ran fast take more elements.  One add per
@@ -47,12 +50,15 @@
 // (its members have higher as well as lower indices); it is bounded by a time
 // budget (PCompArgs::fallbackTicks), after which the workgroup counts L's
 // element itself from the input (an extra read on this slow path only) and
-// goes on.  Every other wait is the look-back on LOWER members of E's team.
-// Members are numbered by START TICKET (takeTicket, device.h: one atomic per
-// workgroup at its start), not by blockIdx, so a lower member is a workgroup
-// that had already started when this one took its ticket: whatever order the
-// hardware dispatches in (MI355X_MICROARCH.md: undefined), no wait is ever on
-// a workgroup that is not resident (by induction over rounds and members).  Another kernel holding CUs
+// goes on.  Every other wait is the look-back on LOWER members of E's team
+// and the log read (written by member 0).  Members are numbered by START
+// TICKET (takeTicket, device.h: one atomic per workgroup at its start, on its
+// team's counter), not by blockIdx, so a lower member is a workgroup that had
+// already started when this one took its ticket: whatever order the hardware
+// dispatches in (MI355X_MICROARCH.md: undefined), no wait is ever on a
+// workgroup that is not resident (by induction over rounds and members).  A
+// grid-wide ticket instead scattered the teams over XCDs (c2 +11 us).
+// Another kernel holding CUs
 // (a second compress on another stream, an RCCL collective) therefore delays
 // the call but cannot stall it.  The look-back is still bounded by a poll cap
 // (a kernel argument); a look-back that runs out POISONS the element instead
@@ -112,11 +118,11 @@ struct PCompArgs {
   uint64_t* ctr;         // [2] element dequeue counters, this call's at epoch & 1 (sync arena)
   uint64_t* elog;        // [teams][maxR] element of each team's round, epoch << 32 | element (sync arena)
   uint32_t maxR;         // rounds a team may take
-  uint32_t slotSpan;     // workgroups per dispatch slot (the CU count): slot ~ ticket / slotSpan
+  uint32_t slotSpan;     // workgroups per dispatch slot (the CU count): slot = blockIdx / slotSpan
   uint32_t epoch;
   uint32_t spinCap;      // polls per look-back before poisoning
   uint32_t fallbackTicks;  // team-barrier wait (100 MHz ticks) before counting the element itself
-  uint32_t* ticket;      // start-ticket counter (takeTicket, device.h; sync arena)
+  uint32_t* ticket;      // [teams] start-ticket counters (takeTicket, device.h; sync arena)
   uint32_t skew;         // test hook: emulated out-of-order dispatch (takeTicket)
   int pb;
   bool useChecksum;
@@ -224,16 +230,21 @@ __global__ __launch_bounds__(pc::kThreads) __attribute__((amdgpu_waves_per_eu(4,
   __shared__ __attribute__((aligned(16))) uint32_t cwE[pc::kBlocksPerItem];
   __shared__ __attribute__((aligned(16))) uint32_t flE[pc::kBlocksPerItem];
   __shared__ __attribute__((aligned(16))) uint32_t preE[pc::kBlocksPerItem];
-  __shared__ uint32_t poisonS, sigS, fbS, vbS;
+  __shared__ uint32_t poisonS, sigS, fbS;
 
   const uint32_t tid = threadIdx.x;
-  // This workgroup's place in the grid is its START TICKET, not blockIdx.x:
-  // team membership, member order and the dispatch-slot priority derive from
-  // it, so "a lower member" is always a workgroup that has already started
-  // and the look-backs and the log read below never wait on one that has not
-  // been dispatched, whatever order the hardware dispatches in.
-  if (tid == 0) vbS = takeTicket(A().ticket, A().grid, A().skew);
-  uint32_t vb = 0;  // set after the first barrier
+  // Team T from blockIdx.x, member X from the team's start-ticket counter;
+  // vb = the (T, X) pair in the blockIdx layout teamX decodes.  Handed to the
+  // other waves in ckS[0] (free until the first window): a new LDS variable
+  // shifted the kernel's LDS layout and cost c2 several microseconds.
+  if (tid == 0) {
+    const PCompArgs ka = A();
+    const uint32_t bid = blockIdx.x;
+    const uint32_t T = ka.xcdTeams ? ((bid >> 3) / ka.team) * 8 + (bid & 7u) : bid / ka.team;
+    const uint32_t X = takeTicket(ka.ticket + T, ka.team, ka.skew);
+    ckS[0] = ka.xcdTeams ? (bid & 7u) + 8 * (((bid >> 3) / ka.team) * ka.team + X) : T * ka.team + X;
+  }
+  uint32_t vb = 0;
   // the lane's half (0: lanes 0-31, 1: lanes 32-63), recomputed at each use
   // by three VALU instructions: held live across the pipeline it spills, and
   // a reload's vmcnt wait drains the input loads in flight
@@ -737,7 +748,7 @@ __global__ __launch_bounds__(pc::kThreads) __attribute__((amdgpu_waves_per_eu(4,
   if (blockIdx.x == 0 && tid == 0)
     __hip_atomic_store(G(A().ctr) + ((A().epoch + 1) & 1u), 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();  // histogram zeroed, ticket in
-  vb = readfirst(vbS);
+  vb = readfirst(ckS[0]);
   uint32_t round = 0;
   uint32_t iE = A().items, iL = itemOfElem(elemOfRound(0));
   if (iL >= A().items) return;
@@ -751,7 +762,7 @@ __global__ __launch_bounds__(pc::kThreads) __attribute__((amdgpu_waves_per_eu(4,
     // launch); rotating gives each slot each level in turn.  (The hand-off
     // window runs above all of them.)
     {
-      const uint32_t pr = (vb / A().slotSpan + round) % 3u;
+      const uint32_t pr = (blockIdx.x / A().slotSpan + round) % 3u;
       if (pr == 0) __builtin_amdgcn_s_setprio(0);
       else if (pr == 1) __builtin_amdgcn_s_setprio(1);
       else __builtin_amdgcn_s_setprio(2);

@@ -184,25 +184,22 @@ __device__ __forceinline__ void sparseCountTile(const BatchDesc& in, gp<uint8_t>
 // histogram(s) (the compacted list's symbols, the n-2 slot included) and
 // added into row tile % nRows of [segments][nb][nRows][256] (PartialHist,
 // zeroed by the host), so the dense codec skips its histogram pass over the
-// list; and the element's last tile to arrive (NormArgs::arrive, the counter
-// hand-off of k_hist) normalises the rows into the encode table and pdf, so
-// the dense codec skips its normalisation launch too (c4 1 x 15M fp32).
+// list.  (Normalising in the element's last-arriving tile instead of the
+// dense codec's k_normalize launch made every tile pay a store drain and a
+// counter round trip: c4 1 x 15M fp32 compress 70 -> 95 us.)
 template <int FT, bool kVec, bool kHist>
 __global__ __launch_bounds__(kThreads) void k_sparseCount(BatchDesc in, BatchDesc outD,
                                                           uint32_t batchOffset, uint32_t numInBatch,
                                                           uint32_t tilesPerElem,
                                                           uint32_t* __restrict__ tileCounts,
                                                           WordOf<FT>* __restrict__ staging,
-                                                          uint32_t* __restrict__ histRows, uint32_t nRows,
-                                                          NormArgs na) {
+                                                          uint32_t* __restrict__ histRows, uint32_t nRows) {
   using W = WordOf<FT>;
   constexpr int kSegs = FloatTraits<FT>::kSegs;
   constexpr uint32_t kCols = 4;  // LDS counter columns per bin (lane & 3)
   __shared__ __attribute__((aligned(16))) W buf[kTileWords];
   __shared__ __attribute__((aligned(16))) uint32_t hs[kHist ? kSegs : 1][kHist ? kNumSymbols * kCols : 4];
   __shared__ uint32_t waveCnt[kWaves];
-  __shared__ uint32_t arriveS;
-  static_assert(sizeof(buf) >= kNumSymbols * 4 + kThreads * 16 + 64, "normalisation scratch in buf");
   const uint32_t b = batchOffset + blockIdx.y;
   const uint32_t n = in.size(b);
   const uint32_t tile = blockIdx.x;
@@ -215,17 +212,6 @@ __global__ __launch_bounds__(kThreads) void k_sparseCount(BatchDesc in, BatchDes
   } else {
     sparseCountTile<FT, kVec, kHist>(in, o, b, n, tile, numInBatch, tilesPerElem, tileCounts, staging, histRows,
                                      nRows, buf, hs, waveCnt);
-  }
-  if constexpr (kHist) {
-    // every tile arrives (empty ones too); the last normalises the element
-    if (na.arrive && lastArrival(na.arrive + b, tilesPerElem, &arriveS)) {
-      uint32_t* scratch = reinterpret_cast<uint32_t*>(&buf[0]);
-      for (int sg = 0; sg < kSegs; ++sg) {
-        normalizeElement(na, numInBatch, b, sg, scratch, scratch + kNumSymbols,
-                         reinterpret_cast<u32x4*>(scratch + kNumSymbols + 16));
-        __syncthreads();
-      }
-    }
   }
 }
 
@@ -407,57 +393,37 @@ void sparseCompressT(StackDeviceMemory& res, const FloatCompressConfig& config, 
   lists.sizes = listLen.data();
   // the list's symbol histogram, counted here for a single element when the
   // three-kernel dense path follows (the single-pass compressor counts as it
-  // loads), and normalised by the element's last tile: the dense codec then
-  // runs k_encode alone (c4 1 x 15M fp32: compress 85 -> 75 us for the
-  // histogram; the normalisation launch ~7 us more).  It lengthens every
-  // tile's workgroup, so with more elements the separate k_hist over the
-  // compacted lists is faster (5 x 15M: 155 us against 170).
+  // loads): the dense codec then skips its histogram pass (c4 1 x 15M fp32:
+  // compress 85 -> 75 us).  It lengthens every tile's workgroup, so with
+  // more elements the separate k_hist over the compacted lists is faster
+  // (5 x 15M: 155 us against 170).
   const bool countHist = nb == 1 && (FT == 4 || !persistentFits(maxN));
   constexpr int kSegs = FloatTraits<FT>::kSegs;
   // histogram rows: up to 64 per element, accumulated with atomics
   const uint32_t G = tiles;
   const uint32_t R = std::min(tiles, kReduceRows);
   auto hist = res.alloc<uint32_t>(s, countHist ? size_t(kSegs) * nb * R * kNumSymbols : 1);
-  auto table = res.alloc<uint4>(s, countHist ? size_t(kSegs) * nb * kNumSymbols : 1);
-  auto pdf = res.alloc<uint16_t>(s, countHist ? size_t(kSegs) * nb * kNumSymbols : 1);
-  if (countHist) HIP_CHECK(hipMemsetAsync(hist.data(), 0, size_t(kSegs) * nb * R * kNumSymbols * 4, s));
-  {
-    // last-arrival counters of the normalising tile (self-resetting); the
-    // lease ends before the dense codec takes its own
-    const size_t regions[kSyncRegions] = {0, 0, 0, 0, size_t(nb) * 4};
-    SyncLease lease(res, s, regions);
-    NormArgs na{};
-    na.in = in;
-    na.hist = hist.data();
-    na.rows = R;
-    na.pb = config.ansConfig.probBits;
-    na.table = table.data();
-    na.pdf = pdf.data();
-    na.arrive = countHist ? static_cast<uint32_t*>(lease.base[kSyncArrive]) : nullptr;
-    na.totalFromHist = true;
-    for (uint32_t y0 = 0; y0 < nb; y0 += kMaxGridY) {
-      const uint32_t ny = std::min(kMaxGridY, nb - y0);
-      prof::Scope p("sparse", s);
-      auto launch = [&](auto vecTag, auto histTag) {
-        k_sparseCount<FT, decltype(vecTag)::value, decltype(histTag)::value><<<dim3(G, ny), kThreads, 0, s>>>(
-            in, outD, y0, nb, tiles, tileCounts.data(), staging.data(), hist.data(), R, na);
-      };
-      if (inAligned16) {
-        if (countHist) launch(std::true_type{}, std::true_type{});
-        else launch(std::true_type{}, std::false_type{});
-      } else {
-        if (countHist) launch(std::false_type{}, std::true_type{});
-        else launch(std::false_type{}, std::false_type{});
-      }
-      HIP_LAUNCH_CHECK();
-      k_sparseGather<FT><<<dim3(tiles, ny), kThreads, 0, s>>>(in, y0, tiles, tileCounts.data(), listLen.data(),
-                                                               staging.data(), lists);
-      HIP_LAUNCH_CHECK();
+  if (countHist) zeroAsync(hist.data(), size_t(kSegs) * nb * R * kNumSymbols * 4, s);
+  for (uint32_t y0 = 0; y0 < nb; y0 += kMaxGridY) {
+    const uint32_t ny = std::min(kMaxGridY, nb - y0);
+    prof::Scope p("sparse", s);
+    auto launch = [&](auto vecTag, auto histTag) {
+      k_sparseCount<FT, decltype(vecTag)::value, decltype(histTag)::value><<<dim3(G, ny), kThreads, 0, s>>>(
+          in, outD, y0, nb, tiles, tileCounts.data(), staging.data(), hist.data(), R);
+    };
+    if (inAligned16) {
+      if (countHist) launch(std::true_type{}, std::true_type{});
+      else launch(std::true_type{}, std::false_type{});
+    } else {
+      if (countHist) launch(std::false_type{}, std::true_type{});
+      else launch(std::false_type{}, std::false_type{});
     }
+    HIP_LAUNCH_CHECK();
+    k_sparseGather<FT><<<dim3(tiles, ny), kThreads, 0, s>>>(in, y0, tiles, tileCounts.data(), listLen.data(),
+                                                             staging.data(), lists);
+    HIP_LAUNCH_CHECK();
   }
-  PartialHist pre{hist.data(), R};
-  pre.table = table.data();
-  pre.pdf = pdf.data();
+  const PartialHist pre{hist.data(), R};
   floatCompressDescs(res, config, nb, lists, maxN, denseOut, outSize_dev, s, nullptr, true,
                      countHist ? &pre : nullptr, sparseN);
 }

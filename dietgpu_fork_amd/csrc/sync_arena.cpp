@@ -57,12 +57,12 @@ SyncLease::SyncLease(StackDeviceMemory& res, hipStream_t stream, const size_t (&
   HIP_CHECK(hipStreamIsCapturing(stream, &cs));
   if (cs != hipStreamCaptureStatusNone) {
     // graph capture: per-call state from the caller's arena, zeroed by a
-    // captured memset on every replay
+    // captured zeroing kernel (zeroAsync) on every replay
     capturing = true;
     size_t total = 0;
     for (int k = 0; k < kSyncRegions; ++k) total += roundUp64(std::max<size_t>(bytes[k], 8), 256);
     capMem_ = res.alloc<uint8_t>(stream, total);
-    HIP_CHECK(hipMemsetAsync(capMem_.data(), 0, total, stream));
+    zeroAsync(capMem_.data(), total, stream);
     size_t off = 0;
     for (int k = 0; k < kSyncRegions; ++k) {
       base[k] = capMem_.data() + off;
@@ -93,21 +93,21 @@ SyncLease::SyncLease(StackDeviceMemory& res, hipStream_t stream, const size_t (&
       while (want < bytes[k]) want *= 2;
       if (a->ptr[k]) HIP_CHECK(hipFree(a->ptr[k]));
       HIP_CHECK(hipMalloc(&a->ptr[k], want));
-      HIP_CHECK(hipMemsetAsync(a->ptr[k], 0, want, stream));
+      zeroAsync(a->ptr[k], want, stream);
       a->bytes[k] = want;
       if (k == kSyncCounters) a->ctrDirty = 0;
     }
   }
   a->epoch = (a->epoch + 1) & kEpochMask;
   if (a->epoch == 0) {  // wrapped: words of every older epoch must go
-    for (int k = 0; k < kSyncRegions; ++k) HIP_CHECK(hipMemsetAsync(a->ptr[k], 0, a->bytes[k], stream));
+    for (int k = 0; k < kSyncRegions; ++k) zeroAsync(a->ptr[k], a->bytes[k], stream);
     a->epoch = 1;
     a->ctrDirty = 0;
   }
   if (dequeue) {  // a k_pcompress call: its counter must start at zero
     const uint32_t mine = a->epoch & 1u;
     if (a->ctrDirty & (1u << mine))
-      HIP_CHECK(hipMemsetAsync(static_cast<uint64_t*>(a->ptr[kSyncCounters]) + mine, 0, sizeof(uint64_t), stream));
+      zeroAsync(static_cast<uint64_t*>(a->ptr[kSyncCounters]) + mine, sizeof(uint64_t), stream);
     a->ctrDirty = 1u << mine;  // the kernel zeroes the other one
   }
   for (int k = 0; k < kSyncRegions; ++k) base[k] = a->ptr[k];

@@ -14,7 +14,7 @@
 //
 // Under hipGraph stream capture every replay would reuse the captured epoch,
 // so a capturing call takes its flags from the caller's StackDeviceMemory
-// instead and zeroes them with a captured memset (a graph node that re-runs
+// instead and zeroes them with a captured zeroing kernel (a graph node that re-runs
 // on every replay); epoch 1.
 #pragma once
 

@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <algorithm>
 #include <cstring>
 
 #include "common.h"
@@ -29,7 +30,25 @@ struct TableChunk {
 __global__ __launch_bounds__(256) void k_table(uint32_t* __restrict__ dst, TableChunk c) {
   for (uint32_t i = threadIdx.x; i < c.n; i += 256) dst[i] = c.w[i];
 }
+__global__ __launch_bounds__(256) void k_zero(uint8_t* __restrict__ dst, size_t bytes) {
+  const size_t stride = size_t(gridDim.x) * 256;
+  const size_t i0 = size_t(blockIdx.x) * 256 + threadIdx.x;
+  if ((reinterpret_cast<uintptr_t>(dst) | bytes) % 16 == 0) {
+    uint4* d = reinterpret_cast<uint4*>(dst);
+    for (size_t i = i0; i < bytes / 16; i += stride) d[i] = make_uint4(0, 0, 0, 0);
+  } else {
+    for (size_t i = i0; i < bytes; i += stride) dst[i] = 0;
+  }
+}
 }  // namespace
+
+void zeroAsync(void* dst, size_t bytes, hipStream_t s) {
+  if (bytes == 0) return;
+  const size_t units = (reinterpret_cast<uintptr_t>(dst) | bytes) % 16 == 0 ? bytes / 16 : bytes;
+  const uint32_t grid = uint32_t(std::min<size_t>(1024, (units + 255) / 256));
+  k_zero<<<grid, 256, 0, s>>>(static_cast<uint8_t*>(dst), bytes);
+  HIP_LAUNCH_CHECK();
+}
 
 // Returns false (nothing enqueued) when the table is not a whole number of
 // aligned 4 B words or is larger than kMaxLaunches chunks.

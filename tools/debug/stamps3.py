@@ -40,9 +40,14 @@ used = st[:, :, 0, 0] > 0
 t0 = st[st > 0].min()
 us = np.where(st > 0, (st - t0) / 100.0, np.nan)  # s_memrealtime: 100 MHz
 print(f"workgroups with stamps: {int(used[:, 0].sum())}; kernel span {np.nanmax(us):.1f} us")
-names = {0: "top", 1: "segs", 2: "syncA", 8: "pubH", 3: "split", 4: "wait", 5: "syncB", 10: "parts", 6: "place",
-         7: "norm", 9: "syncC"}
-order = [0, 1, 2, 8, 3, 4, 5, 10, 6, 7, 9]
+import os as _os
+if _os.environ.get("STAMP4"):
+    names = {0: "top", 1: "segs", 2: "pubH", 10: "deq", 3: "gath", 4: "sig", 5: "norm", 6: "lb", 7: "plc0", 8: "plc1", 9: "syncC"}
+    order = [0, 1, 2, 10, 3, 4, 5, 6, 7, 8, 9]
+else:
+    names = {0: "top", 1: "segs", 2: "syncA", 8: "pubH", 3: "split", 4: "wait", 5: "syncB", 10: "parts", 6: "place",
+             7: "norm", 9: "syncC"}
+    order = [0, 1, 2, 8, 3, 4, 5, 10, 6, 7, 9]
 for it in range(8):
     m = used[:, it]
     if not m.any():

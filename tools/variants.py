@@ -125,7 +125,54 @@ XW = [("encode.h", """  uint32_t dst;
   (void)trashAddr;
   asm volatile("s_and_saveexec_b64 %0, %1\n\tds_write_b16 %2, %3\n\ts_mov_b64 exec, %0"
                : "=&s"(sav_) : "s"(vote), "v"(ringAddr), "v"(p.x) : "memory", "scc");""")]
+# round 4: member index from blockIdx (round 3) instead of the per-team start ticket
+BIDX = [(P, "    memberS = takeTicket(ka.ticket + T, ka.team, ka.skew);",
+         "    memberS = ka.xcdTeams ? (bid >> 3) % ka.team : bid % ka.team;")]
+XREAD = "    X = readfirst(*(volatile uint32_t*)&memberS);"
+BIDX0 = [(P, XREAD, "    X = ka.xcdTeams ? (bid >> 3) % ka.team : bid % ka.team;")]
+SGPRX = [(P, XREAD, "    X = memberX;"),
+         (P, "  auto teamX = [&](uint32_t& T, uint32_t& X) __attribute__((always_inline)) {",
+             "  uint32_t memberX = 0;\n  auto teamX = [&](uint32_t& T, uint32_t& X) __attribute__((always_inline)) {"),
+         (P, "  uint32_t round = 0;\n", "  memberX = readfirst(memberS);\n  uint32_t round = 0;\n")]
+W2BIDX = [(P, "    X = memberX;", "    X = ka.xcdTeams ? (bid >> 3) % ka.team : bid % ka.team;")]
+NOZERO = [("upload.hip", """__global__ __launch_bounds__(256) void k_zero(uint8_t* __restrict__ dst, size_t bytes) {
+  const size_t stride = size_t(gridDim.x) * 256;
+  const size_t i0 = size_t(blockIdx.x) * 256 + threadIdx.x;
+  if ((reinterpret_cast<uintptr_t>(dst) | bytes) % 16 == 0) {
+    uint4* d = reinterpret_cast<uint4*>(dst);
+    for (size_t i = i0; i < bytes / 16; i += stride) d[i] = make_uint4(0, 0, 0, 0);
+  } else {
+    for (size_t i = i0; i < bytes; i += stride) dst[i] = 0;
+  }
+}
+""", ""), ("upload.hip", """  const size_t units = (reinterpret_cast<uintptr_t>(dst) | bytes) % 16 == 0 ? bytes / 16 : bytes;
+  const uint32_t grid = uint32_t(std::min<size_t>(1024, (units + 255) / 256));
+  k_zero<<<grid, 256, 0, s>>>(static_cast<uint8_t*>(dst), bytes);
+  HIP_LAUNCH_CHECK();""", """  HIP_CHECK(hipMemsetAsync(dst, 0, bytes, s));""")]
+# per-wave phase stamps of the round-4 window (two wave chains)
+STAMP4 = [
+    (P, "namespace pc {", "__device__ unsigned long long g_stamp[4096 * 8 * 4 * 16];\n#define STAMP(ph) do { if (laneNow() == 0 && itc < 8) { unsigned long long t_ = __builtin_amdgcn_s_memrealtime(); asm volatile(\"\" : \"+v\"(t_)); ((volatile unsigned long long*)g_stamp)[((blockIdx.x * 8 + itc) * 4 + w) * 16 + (ph)] = t_; } } while (0)\nnamespace pc {"),
+    (P, "  uint32_t round = 0;\n", "  uint32_t round = 0;\n  uint32_t itc = 0;\n"),
+    (P, "    // Segment-phase wave priority rotates", "    STAMP(0);\n    // Segment-phase wave priority rotates"),
+    (P, "    __builtin_amdgcn_s_setprio(3);\n", "    STAMP(1);\n    __builtin_amdgcn_s_setprio(3);\n"),
+    (P, "      publishHist(itemOf(iL, A(), IN()));\n", "      publishHist(itemOf(iL, A(), IN()));\n      STAMP(2);\n"),
+    (P, "      if (w != 1) markReady();", "      STAMP(3);\n      if (w != 1) markReady();"),
+    (P, "        uint32_t ckL = kCk ? waveXor(ckAcc) : 0u;", "        STAMP(4);\n        uint32_t ckL = kCk ? waveXor(ckAcc) : 0u;"),
+    (P, "        *(lp<u32x2>)&pdfS[4 * lane] =", "        STAMP(5);\n        *(lp<u32x2>)&pdfS[4 * lane] ="),
+    (P, "      if (hasE) lookBackE(itemOf(iE, A(), IN()));\n", "      if (hasE) lookBackE(itemOf(iE, A(), IN()));\n      STAMP(6);\n"),
+    (P, "      place(itemOf(iE, A(), IN()));\n", "      STAMP(7);\n      place(itemOf(iE, A(), IN()));\n      STAMP(8);\n"),
+    (P, "    // the next round's element (nextS, wave 3)", "    STAMP(9);\n    // the next round's element (nextS, wave 3)"),
+    (P, "      nextS = elemOfRound(round + 1);\n", "      nextS = elemOfRound(round + 1);\n      STAMP(10);\n"),
+    (P, "    iE = iL;\n", "    ++itc;\n    iE = iL;\n"),
+    ("codec.hip", "uint32_t deviceErrorCount(bool reset) {", "extern \"C\" void* dietgpu_debug_stamps() { void* p = nullptr; (void)hipGetSymbolAddress(&p, HIP_SYMBOL(g_stamp)); return p; }\n\nuint32_t deviceErrorCount(bool reset) {"),
+]
 VARS = {
+    "stamp4": STAMP4,
+    "nozero": NOZERO,
+    "w2bidx": W2BIDX,
+    "bidx0": BIDX0,
+    "sgprx": SGPRX,
+    "bidx": BIDX,
     "hcl": [(P, "lp<uint32_t> hcol = (lp<uint32_t>)&hist[l % pc::kHistCols];", "lp<uint32_t> hcol = (lp<uint32_t>)&hist[laneNow() % pc::kHistCols];")],
     "hcx": [(P, "lp<uint32_t> hcol = (lp<uint32_t>)&hist[l % pc::kHistCols];", "lp<uint32_t> hcol = (lp<uint32_t>)&hist[(l + (halfNow() ? 6u : 0u)) % pc::kHistCols];")],
     "dp1": [("codec.hip", "constexpr uint32_t kMaxDecodeChunks = 8;", "constexpr uint32_t kMaxDecodeChunks = 1;")],
