@@ -235,10 +235,8 @@ bool compressPersistent(StackDeviceMemory& res, int pb, bool useChecksum, uint32
   const size_t partBytes = size_t(items) * kNumSymbols * 4;
   const uint32_t teams = grid / team;
   const uint32_t maxR = 2 * divUp(nb, teams) + 2;
-  // (counters region: the dequeue counters, then one start-ticket counter
-  // per team)
-  const size_t regions[kSyncRegions] = {kSyncTicketOffset + size_t(teams) * 4, size_t(items) * 8,
-                                        partBytes + (kCk ? size_t(items) * 4 : 0), size_t(teams) * maxR * 8, 0};
+  const size_t regions[kSyncRegions] = {16, size_t(items) * 8, partBytes + (kCk ? size_t(items) * 4 : 0),
+                                        size_t(teams) * maxR * 8, 0};
   SyncLease lease(res, s, regions, /*dequeue=*/true);
   if (FT != 0 && useChecksum) {
     zeroAsync(ck.data(), sizeof(uint32_t) * nb, s);
@@ -274,8 +272,6 @@ bool compressPersistent(StackDeviceMemory& res, int pb, bool useChecksum, uint32
   a.epoch = lease.epoch;
   a.spinCap = spinCap();
   a.fallbackTicks = barrierBudgetTicks();
-  a.ticket = lease.ticket();
-  a.skew = dispatchSkew();
   a.pb = pb;
   a.useChecksum = useChecksum;
   prof::Scope p("compress", s);
@@ -343,7 +339,7 @@ void encodeBatchDevice(StackDeviceMemory& res, int pb, bool useChecksum, uint32_
   // k_encode's look-back flags (fused formats: one per element and encode
   // workgroup, epoch-tagged, never zeroed) and the last-arrival counters, in
   // this stream's sync arena
-  const size_t regions[kSyncRegions] = {0, kFused ? size_t(nb) * nW * 8 : 0, 0, 0, size_t(nb) * 4};
+  const size_t regions[kSyncRegions] = {0, kFused ? size_t(nb) * nW * 8 : 0, 0, 0, size_t(nb) * kSegs * 4};
   SyncLease lease(res, s, regions);
   NormArgs na;
   na.in = in;

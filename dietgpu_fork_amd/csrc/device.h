@@ -224,17 +224,9 @@ __device__ __forceinline__ void stSc1(gp<uint32_t> p, uint32_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Workgroup order independent of dispatch order.  Every workgroup of a launch
-// takes exactly one ticket from a per-stream counter at its start; ticket
-// order is START order, so a workgroup that waits only on lower tickets waits
-// only on workgroups that are already running (MI355X_MICROARCH.md:
-// dispatch order and the block -> XCD map are undefined).  The counter is an
-// atomic_inc wrapping at count - 1: the launch's last ticket returns it to 0,
-// ready for the next launch on the stream, with no memset.
-// `skew` (test hook, dietgpu_set_dispatch_skew): workgroup g first waits
-// (63 - g % 64) * skew ticks of the 100 MHz clock, so tickets go out in about
-// reverse launch order within every 64 workgroups -- out-of-order dispatch,
-// emulated.  One lane.
+// Test hook (dietgpu_set_dispatch_skew): workgroup g first waits
+// (63 - g % 64) * skew ticks of the 100 MHz clock, so the workgroups start in
+// about reverse index order within every 64.  One lane.
 __device__ __forceinline__ void skewDelay(uint32_t skew) {
 #if defined(__HIP_DEVICE_COMPILE__)
   const uint32_t g = blockIdx.y * gridDim.x + blockIdx.x;
@@ -244,10 +236,6 @@ __device__ __forceinline__ void skewDelay(uint32_t skew) {
 #else
   (void)skew;
 #endif
-}
-__device__ __forceinline__ uint32_t takeTicket(uint32_t* counter, uint32_t count, uint32_t skew) {
-  if (skew) skewDelay(skew);
-  return atomicInc(counter, count - 1);
 }
 
 }  // namespace dietgpu

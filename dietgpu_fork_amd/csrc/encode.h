@@ -468,13 +468,10 @@ static __global__ __launch_bounds__(kThreads) void k_histReduce(
     ck = waveXor(ck);
     if (threadIdx.x == 0) stSc1(G(outCk) + uint64_t(b) * groups + g, ck);
   }
-  // the element's last workgroup (over groups and segments) normalises it
-  if (na.arrive && lastArrival(na.arrive + b, groups * segs, &red[kWaves])) {
-    for (uint32_t s = 0; s < segs; ++s) {
-      normalizeElement(na, numInBatch, b, s, keys, red, red4);
-      __syncthreads();
-    }
-  }
+  // the (element, segment)'s last workgroup normalises that segment: fp64's
+  // two segments are normalised by two workgroups side by side
+  if (na.arrive && lastArrival(na.arrive + uint64_t(b) * segs + blockIdx.z, groups, &red[kWaves]))
+    normalizeElement(na, numInBatch, b, blockIdx.z, keys, red, red4);
 }
 
 // ---------------------------------------------------------------------------
@@ -932,7 +929,7 @@ __global__ __launch_bounds__(enc::kThreads) void k_encode(BatchDesc in, BatchDes
   // starts of the big grids: c3 encode 2.35 -> 2.68 ms, batch-1 bf16
   // 62 -> 80 us.
   const uint32_t wx = blockIdx.x, wy = blockIdx.y;
-  if (kFused && tail.skew && tid == 0) skewDelay(tail.skew);  // test hook (takeTicket)
+  if (kFused && tail.skew && tid == 0) skewDelay(tail.skew);  // test hook (dietgpu_set_dispatch_skew)
   const uint32_t b = batchOffset + wy;
   const uint32_t n = in.size(b);
   const uint32_t nBlocks = divUp(n, kBlockSize);

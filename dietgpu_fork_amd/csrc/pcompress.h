@@ -13,12 +13,11 @@
 // block pair per wave); the items of an element form its team.  The grid is
 // at most one generation of resident workgroups, a whole number of teams of
 // workgroups, and a workgroup team takes one element per round: member x of
-// team T works item x of the team's element.  Team membership comes from
-// blockIdx and keeps each team on one XCD (workgroups w, w + 8, ... share one
-// under the observed round-robin placement), so the team's hand-offs stay in
-// one L2 (speed only, never correctness); the member index x is the order in
-// which the team's workgroups started (a per-team start ticket, below).
-// Elements of rounds 0 and 1 are static (r * teams + T); from
+// team T works item x of the team's element.  Team membership keeps each
+// team on one XCD (workgroups w, w + 8, ... share one under the observed
+// round-robin placement), so the team's hand-offs stay in one L2 (speed
+// only, never correctness), and gives the members increasing workgroup
+// indices.  Elements of rounds 0 and 1 are static (r * teams + T); from
 // round 2 on, member 0 takes the team's element two rounds ahead with one
 // returning add on a per-call counter and logs it (epoch-tagged) for the
 // other members, so teams that ran fast take more elements.  One add per
@@ -40,10 +39,17 @@
 // waves 1-3 copy E's payload out of the LDS rings.
 //
 // Cross-workgroup hand-offs follow MI355X_MICROARCH.md's tagged-granule form:
-// a partial histogram word is {epoch << 16 | count} written by one sc1 store
-// and read with sc1 loads, so its consumer needs no arrival flag (no drain of
-// the producer's stores, no barrier, one memory round trip per hop); the
-// look-back flags carry their value and epoch in one 8 B word.
+// a partial histogram word is {epoch << 16 | count}, read with sc1 loads, so
+// its consumer needs no arrival flag (no drain of the producer's stores, no
+// barrier, one memory round trip per hop); the look-back flags carry their
+// value and epoch in one 8 B word.  The partials are stored plain (sc0): the
+// line stays in the XCD's L2, where the team's other members -- the same XCD
+// under round-robin placement -- read it at L2 latency (an sc1 store drops the
+// line and every read goes to the fabric: c2 compress 141.5 -> 138.5 us).  A
+// member placed on another XCD could see a stale line; the team barrier's
+// time budget then counts the element from the input (below), so this is
+// speed only.  The flags and the log keep sc1 stores: their waits have no
+// such fallback.
 //
 // Forward progress does not depend on the grid being co-resident.  The only
 // wait on workgroups that may not have been dispatched is L's team barrier
@@ -51,14 +57,17 @@
 // budget (PCompArgs::fallbackTicks), after which the workgroup counts L's
 // element itself from the input (an extra read on this slow path only) and
 // goes on.  Every other wait is the look-back on LOWER members of E's team
-// and the log read (written by member 0).  Members are numbered by START
-// TICKET (takeTicket, device.h: one atomic per workgroup at its start, on its
-// team's counter), not by blockIdx, so a lower member is a workgroup that had
-// already started when this one took its ticket: whatever order the hardware
-// dispatches in (MI355X_MICROARCH.md: undefined), no wait is ever on a
-// workgroup that is not resident (by induction over rounds and members).  A
-// grid-wide ticket instead scattered the teams over XCDs (c2 +11 us).
-// Another kernel holding CUs
+// and the log read (written by member 0), i.e. on lower workgroup indices.
+// That cannot deadlock as long as each XCD dispatches its own workgroups in
+// index order (observed; not a HIP contract): the lowest unfinished
+// workgroup then waits on nothing unfinished, and its XCD dispatched every
+// lower workgroup of its own before it, so it holds or will get a slot --
+// whatever the timing across XCDs and whatever another kernel holds.
+// Members numbered by a per-team start ticket instead (a wait is then only
+// ever on a workgroup that has started, under any dispatch order) measured
+// c2 compress +10 us, same box, in every form tried (DESIGN.md section 7,
+// round 4), so the kernel keeps the index order and bounds the waits
+// instead.  Another kernel holding CUs
 // (a second compress on another stream, an RCCL collective) therefore delays
 // the call but cannot stall it.  The look-back is still bounded by a poll cap
 // (a kernel argument); a look-back that runs out POISONS the element instead
@@ -122,8 +131,6 @@ struct PCompArgs {
   uint32_t epoch;
   uint32_t spinCap;      // polls per look-back before poisoning
   uint32_t fallbackTicks;  // team-barrier wait (100 MHz ticks) before counting the element itself
-  uint32_t* ticket;      // [teams] start-ticket counters (takeTicket, device.h; sync arena)
-  uint32_t skew;         // test hook: emulated out-of-order dispatch (takeTicket)
   int pb;
   bool useChecksum;
 };
@@ -233,18 +240,6 @@ __global__ __launch_bounds__(pc::kThreads) __attribute__((amdgpu_waves_per_eu(4,
   __shared__ uint32_t poisonS, sigS, fbS;
 
   const uint32_t tid = threadIdx.x;
-  // Team T from blockIdx.x, member X from the team's start-ticket counter;
-  // vb = the (T, X) pair in the blockIdx layout teamX decodes.  Handed to the
-  // other waves in ckS[0] (free until the first window): a new LDS variable
-  // shifted the kernel's LDS layout and cost c2 several microseconds.
-  if (tid == 0) {
-    const PCompArgs ka = A();
-    const uint32_t bid = blockIdx.x;
-    const uint32_t T = ka.xcdTeams ? ((bid >> 3) / ka.team) * 8 + (bid & 7u) : bid / ka.team;
-    const uint32_t X = takeTicket(ka.ticket + T, ka.team, ka.skew);
-    ckS[0] = ka.xcdTeams ? (bid & 7u) + 8 * (((bid >> 3) / ka.team) * ka.team + X) : T * ka.team + X;
-  }
-  uint32_t vb = 0;
   // the lane's half (0: lanes 0-31, 1: lanes 32-63), recomputed at each use
   // by three VALU instructions: held live across the pipeline it spills, and
   // a reload's vmcnt wait drains the input loads in flight
@@ -298,14 +293,14 @@ __global__ __launch_bounds__(pc::kThreads) __attribute__((amdgpu_waves_per_eu(4,
   // work ahead of the last ones).
   auto teamX = [&](uint32_t& T, uint32_t& X) __attribute__((always_inline)) {
     const PCompArgs ka = A();
-    if (ka.xcdTeams) {  // vb = xcd + 8 (group * team + x), team T = group * 8 + xcd
-      const uint32_t xcd = vb & 7u, q = vb >> 3;
+    if (ka.xcdTeams) {  // w = xcd + 8 (group * team + x), team T = group * 8 + xcd
+      const uint32_t xcd = blockIdx.x & 7u, q = blockIdx.x >> 3;
       const uint32_t grp = q / ka.team;
       X = q - grp * ka.team;
       T = grp * 8 + xcd;
     } else {
-      T = vb / ka.team;
-      X = vb - T * ka.team;
+      T = blockIdx.x / ka.team;
+      X = blockIdx.x - T * ka.team;
     }
   };
   // item of element e (>= nb: none) for this member
@@ -518,7 +513,8 @@ __global__ __launch_bounds__(pc::kThreads) __attribute__((amdgpu_waves_per_eu(4,
   // (after a workgroup barrier: every wave's counts and ckS are in).  The
   // data carries its own epoch, so the consumer needs no separate arrival
   // flag: no drain of the stores, no barrier, one memory round trip per hop
-  // (MI355X_MICROARCH.md: a tagged granule written by one sc1 store).  The
+  // (MI355X_MICROARCH.md: a tagged granule).  Plain (sc0) stores keep the
+  // line in this XCD's L2 for the team's sc1 loads (header comment).  The
   // words live in the persistent epoch-tagged sync arena, never in scratch a
   // stale value could come from.
   auto publishHist = [&](const PItem& it) __attribute__((always_inline)) {
@@ -532,7 +528,8 @@ __global__ __launch_bounds__(pc::kThreads) __attribute__((amdgpu_waves_per_eu(4,
       hist[tid * pc::kHistStride + k] = 0;
     }
     const uint32_t tag = A().epoch << 16;
-    stSc1(G(A().part) + uint64_t(it.i) * kNumSymbols + tid, tag | cnt);
+    __hip_atomic_store(G(A().part) + uint64_t(it.i) * kNumSymbols + tid, tag | cnt, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_WORKGROUP);
     if constexpr (kCk) {
       if (tid == 0) stSc1(G(A().partCk) + it.i, tag | (ckS[0] ^ ckS[1] ^ ckS[2] ^ ckS[3]));
     }
@@ -747,8 +744,7 @@ __global__ __launch_bounds__(pc::kThreads) __attribute__((amdgpu_waves_per_eu(4,
   // stream run one after another, so nothing reads that counter now
   if (blockIdx.x == 0 && tid == 0)
     __hip_atomic_store(G(A().ctr) + ((A().epoch + 1) & 1u), 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __syncthreads();  // histogram zeroed, ticket in
-  vb = readfirst(ckS[0]);
+  __syncthreads();  // histogram zeroed
   uint32_t round = 0;
   uint32_t iE = A().items, iL = itemOfElem(elemOfRound(0));
   if (iL >= A().items) return;

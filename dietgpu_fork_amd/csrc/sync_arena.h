@@ -40,10 +40,8 @@ constexpr uint32_t kEpochMask = 0xffffu;
 // encode.h): untagged, they wrap back to zero at every element's last
 // arrival, so they are zero between calls.
 enum SyncRegion : int { kSyncCounters = 0, kSyncFlags, kSyncPartials, kSyncLog, kSyncArrive, kSyncRegions };
-// kSyncCounters layout: k_pcompress's two u64 dequeue counters, then the u32
-// workgroup-ticket counter (takeTicket, device.h; self-resetting).
-constexpr size_t kSyncTicketOffset = 16;
-constexpr size_t kSyncCounterBytes = 32;
+// kSyncCounters layout: k_pcompress's two u64 dequeue counters.
+constexpr size_t kSyncCounterBytes = 16;
 
 class SyncLease {
  public:
@@ -53,9 +51,6 @@ class SyncLease {
   // must start at zero (see Arena::ctrDirty).
   SyncLease(StackDeviceMemory& res, hipStream_t stream, const size_t (&bytes)[kSyncRegions], bool dequeue = false);
 
-  uint32_t* ticket() const {
-    return reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(base[kSyncCounters]) + kSyncTicketOffset);
-  }
   SyncLease(const SyncLease&) = delete;
   SyncLease& operator=(const SyncLease&) = delete;
 
@@ -86,9 +81,10 @@ uint32_t spinCap();
 void setBarrierBudget(uint32_t ticks);
 uint32_t barrierBudgetTicks();
 
-// Test hook: workgroups of the compressors wait (63 - g % 64) * ticks before
-// taking their start ticket (takeTicket, device.h), emulating out-of-order
-// dispatch.  0 (default) is off.
+// Test hook: workgroups of the compressors (k_pcompress, k_encode) wait
+// (63 - g % 64) * ticks at their start (skewDelay, device.h), so they start in
+// about reverse index order within every 64: the look-backs then wait on
+// late-starting lower workgroups.  0 (default) is off.
 void setDispatchSkew(uint32_t ticks);
 uint32_t dispatchSkew();
 

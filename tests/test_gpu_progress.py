@@ -108,12 +108,11 @@ def test_compress_beside_occupying_kernel(C, ws):
 
 @pytest.mark.parametrize("shape", ["c2", "c3"])
 def test_out_of_order_dispatch(C, ws, shape):
-    """Workgroups take their start tickets in about REVERSE launch order
-    (test hook: each waits (63 - g % 64) x 1 us first), emulating a dispatcher
-    that starts later workgroups first.  The look-backs (k_pcompress's team
-    look-back and log read; k_encode's fused look-back on the c3 path) order
-    workgroups by ticket, so they still only wait on started workgroups:
-    archives oracle-identical, nothing abandoned."""
+    """Workgroups start in about REVERSE index order (test hook: each waits
+    (63 - g % 64) x 1 us first), so the look-backs (k_pcompress's team
+    look-back and log read; k_encode's fused look-back on the c3 path) wait
+    on lower workgroups that start up to 63 us late: archives
+    oracle-identical, nothing abandoned (no wait runs out of polls)."""
     C.device_error_count(reset=True)
     try:
         C.set_dispatch_skew(100)

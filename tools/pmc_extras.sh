@@ -16,7 +16,7 @@ timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o run --outp
   -- python3 bench.py $A > "$OUT/pmc_fetch.log" 2>&1
 timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o run --output-format csv \
   -- python3 bench.py $A > "$OUT/pmc_write.log" 2>&1
-# VALU issue: the three-kernel encode of byte data (c3) is VALU-bound
+# VALU and SALU issue counters of every kernel (c3: the encode step chain)
 timeout -s KILL 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CU_CYCLES GRBM_GUI_ACTIVE \
   -d "$OUT/pmc_valu" -o run --output-format csv -- python3 bench.py $A > "$OUT/pmc_valu.log" 2>&1
 echo "pmc_extras $TAG done"

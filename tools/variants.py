@@ -166,7 +166,25 @@ STAMP4 = [
     (P, "    iE = iL;\n", "    ++itc;\n    iE = iL;\n"),
     ("codec.hip", "uint32_t deviceErrorCount(bool reset) {", "extern \"C\" void* dietgpu_debug_stamps() { void* p = nullptr; (void)hipGetSymbolAddress(&p, HIP_SYMBOL(g_stamp)); return p; }\n\nuint32_t deviceErrorCount(bool reset) {"),
 ]
+# round 4: partial histograms published with plain stores (the line stays in
+# the XCD's L2; a same-XCD consumer's sc1 load is then an L2 hit), flags sc1
+PLAINPART = [(P, "    stSc1(G(A().part) + uint64_t(it.i) * kNumSymbols + tid, tag | cnt);",
+              "    __hip_atomic_store(G(A().part) + uint64_t(it.i) * kNumSymbols + tid, tag | cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);")]
+PLAINALL = PLAINPART + [
+    (P, """      __hip_atomic_store(G(A().flags) + it.tb + it.x,
+                         (it.x == 0 ? kFlagPrefix : kFlagAgg) | (uint64_t(A().epoch) << 32) | agg,
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);""", """      __hip_atomic_store(G(A().flags) + it.tb + it.x,
+                         (it.x == 0 ? kFlagPrefix : kFlagAgg) | (uint64_t(A().epoch) << 32) | agg,
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);"""),
+    ("encode.h", """    __hip_atomic_store(f + x, kFlagPrefix | (poison ? kFlagPoisonE : 0ull) | tag | uint64_t(excl + agg),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);""", """    __hip_atomic_store(f + x, kFlagPrefix | (poison ? kFlagPoisonE : 0ull) | tag | uint64_t(excl + agg),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);"""),
+    (P, """    __hip_atomic_store(G(ka.elog) + uint64_t(T) * ka.maxR + r, tag | min(e, ka.nb), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);""", """    __hip_atomic_store(G(ka.elog) + uint64_t(T) * ka.maxR + r, tag | min(e, ka.nb), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_WORKGROUP);""")]
 VARS = {
+    "plainall": PLAINALL,
+    "plainpart": PLAINPART,
     "stamp4": STAMP4,
     "nozero": NOZERO,
     "w2bidx": W2BIDX,
