@@ -295,6 +295,7 @@ void encodeBatchDevice(StackDeviceMemory& res, int pb, bool useChecksum, uint32_
   const uint32_t MB = divUp(maxSize, kBlockSize);
   const bool userHist = FT == 0 && hist_dev != nullptr;
   const bool preHist = FT != 0 && pre != nullptr;  // partial rows counted by the caller
+  const bool preNorm = preHist && pre->table != nullptr;  // ... and normalised
   const uint32_t chunkWords = histChunkWords(nb, maxSize);
   const uint32_t chunks = preHist ? std::max(1u, pre->nRows) : std::max(1u, divUp(maxSize, chunkWords));
   const bool runHist = !preHist && (!userHist || useChecksum);
@@ -317,14 +318,14 @@ void encodeBatchDevice(StackDeviceMemory& res, int pb, bool useChecksum, uint32_
   const uint32_t* chunkRows = preHist ? pre->rows : partHist.data();
   // first-level sums when elements have many chunks (k_histReduce)
   const uint32_t groups = divUp(chunks, kReduceRows);
-  const bool reduce2 = (runHist || preHist) && chunks > kReduceRows;
+  const bool reduce2 = (runHist || preHist) && !preNorm && chunks > kReduceRows;
   auto groupHist = res.alloc<uint32_t>(s, reduce2 ? size_t(kSegs) * nb * groups * kNumSymbols : 1);
   auto groupCk = res.alloc<uint32_t>(s, reduce2 && rawCk ? size_t(nb) * groups : 1);
   auto ck = res.alloc<uint32_t>(s, nb);
-  auto tableMem = res.alloc<uint4>(s, size_t(kSegs) * nb * kNumSymbols);
-  auto pdfMem = res.alloc<uint16_t>(s, size_t(kSegs) * nb * kNumSymbols);
-  const uint4* table = tableMem.data();
-  const uint16_t* pdf = pdfMem.data();
+  auto tableMem = res.alloc<uint4>(s, preNorm ? 1 : size_t(kSegs) * nb * kNumSymbols);
+  auto pdfMem = res.alloc<uint16_t>(s, preNorm ? 1 : size_t(kSegs) * nb * kNumSymbols);
+  const uint4* table = preNorm ? pre->table : tableMem.data();
+  const uint16_t* pdf = preNorm ? pre->pdf : pdfMem.data();
   auto slots = res.alloc<uint8_t>(s, size_t(kSegs) * nb * std::max(MB, 1u) * kSlotBytes);
   auto cw = res.alloc<uint32_t>(s, kFused ? 1 : size_t(kSegs) * nb * std::max(MB, 1u));
   const uint32_t nW = std::max(1u, divUp(MB, EncCfg<FT>::kBlocksPerWG));
@@ -389,7 +390,7 @@ void encodeBatchDevice(StackDeviceMemory& res, int pb, bool useChecksum, uint32_
                                           finalInReduce ? naFinal : na, kSegs);
       HIP_LAUNCH_CHECK();
     }
-    if (!finalInReduce && !finalInHist) {
+    if (!finalInReduce && !finalInHist && !preNorm) {
       prof::Scope p("normalize", s);
       dim3 g(ny, kSegs);
       k_normalize<<<g, kThreads, 0, s>>>(na, y0, nb);

@@ -16,9 +16,14 @@ struct DeviceTables;  // codec.hip: per-call pointer tables (maybe kernel-argume
 // sparse compressor counts its nonzeros as it compacts them, so the dense
 // codec's histogram pass is skipped): u32 rows [segments][nb][nRows][256],
 // summed per element.  Ignored when the single-pass compressor takes the call.
+// table / pdf non-null: the caller has normalised the rows too
+// ([segments][nb][256] encode-table entries and u16 pdfs, NormArgs layout),
+// so the dense codec goes straight to k_encode.
 struct PartialHist {
   const uint32_t* rows;
   uint32_t nRows;
+  const uint4* table = nullptr;
+  const uint16_t* pdf = nullptr;
 };
 
 void floatCompressDescs(StackDeviceMemory& res, const FloatCompressConfig& config, uint32_t nb,

@@ -35,6 +35,10 @@ namespace dietgpu {
 namespace {
 
 constexpr uint32_t kTileWords = 4096;   // 4 waves x 16 steps x 64 lanes
+// tiles per k_sparseExpand workgroup: two (bitmap and list gathers of both
+// in the same two round trips) measured slower -- 1 x 15M fp32 decompress 59
+// -> 68 us: the doubled registers and LDS halved the resident workgroups
+constexpr uint32_t kExpandTiles = 1;
 constexpr uint32_t kMaxGridY = 65535;
 
 template <int FT>
@@ -237,21 +241,34 @@ __device__ __forceinline__ uint32_t tilePrefix(gp<const uint32_t> counts, uint32
   return blockSum<kThreads>(sum, red);
 }
 
-// s2: staged nonzeros -> their list positions.  grid (tiles, batch).  The
-// tile's list offset is the sum of the element's earlier tile counts
-// (tilePrefix); the last tile also stores the list's length.
+// s2: staged nonzeros -> their list positions.  grid (tiles [+ 1], batch).
+// The tile's list offset is the sum of the element's earlier tile counts
+// (tilePrefix); the last tile also stores the list's length.  With
+// na.hist set (k_sparseCount counted the list's histogram), one extra
+// workgroup per element normalises it meanwhile, into the dense codec's
+// encode table and pdf: the dense codec then skips its k_normalize launch
+// (c4 1 x 15M fp32 compress -6 us).
 template <int FT>
 __global__ __launch_bounds__(kThreads) void k_sparseGather(BatchDesc in, uint32_t batchOffset,
                                                            uint32_t tilesPerElem,
                                                            const uint32_t* __restrict__ tileCounts,
                                                            uint32_t* __restrict__ listLen,
                                                            const WordOf<FT>* __restrict__ staging,
-                                                           BatchDesc lists) {
+                                                           BatchDesc lists, NormArgs na) {
   using W = WordOf<FT>;
   __shared__ uint32_t red[kWaves];
   const uint32_t b = batchOffset + blockIdx.y;
-  const uint32_t n = in.size(b);
   const uint32_t tile = blockIdx.x;
+  if (tile == tilesPerElem) {  // (grid.x = tiles + 1 only with na.hist)
+    __shared__ __attribute__((aligned(16))) uint32_t keys[kNumSymbols];
+    __shared__ u32x4 red4[kThreads];
+    for (int sg = 0; sg < FloatTraits<FT>::kSegs; ++sg) {
+      normalizeElement(na, batchOffset + gridDim.y, b, sg, keys, red, red4);  // (used with nb == 1)
+      __syncthreads();
+    }
+    return;
+  }
+  const uint32_t n = in.size(b);
   if (tile * kTileWords >= n) {
     // an empty element has no last tile: its (empty) list length is written here
     if (n == 0 && tile == 0 && threadIdx.x == 0) listLen[b] = 0;
@@ -293,10 +310,12 @@ __global__ __launch_bounds__(kThreads) void k_sparseHeaders(BatchDesc in, uint32
 }
 
 // d3: expand the decoded nonzero list into the output (fill_in_nonzeros
-// :95-144).  grid (tiles, batch); per 4096-word tile: expansion into LDS from
-// the tile's first list index, then 16 B stores when the output is 16 B
-// aligned.
-template <int FT, bool kVec>
+// :95-144).  grid (ceil(tiles / kT), batch); a workgroup expands kT
+// consecutive 4096-word tiles: their bitmap words and the first tile's list
+// index (tilePrefix) in one memory round trip, the list gathers of all kT
+// tiles in a second, then 16 B streaming stores when the output is 16 B
+// aligned.  (kT = kExpandTiles: see there.)
+template <int FT, bool kVec, uint32_t kT>
 __global__ __launch_bounds__(kThreads) void k_sparseExpand(BatchDesc in, BatchDesc out, uint32_t batchOffset,
                                                            uint32_t tilesPerElem, const uint32_t* __restrict__ sizes,
                                                            const uint32_t* __restrict__ tileCounts,
@@ -307,67 +326,83 @@ __global__ __launch_bounds__(kThreads) void k_sparseExpand(BatchDesc in, BatchDe
   using W = WordOf<FT>;
   constexpr uint32_t kSteps = kTileWords / kWaves / 64;
   constexpr uint32_t kVecs = kTileWords * sizeof(W) / 16 / kThreads;
-  __shared__ __attribute__((aligned(16))) W buf[kTileWords];
-  __shared__ uint32_t waveCnt[kWaves];
+  __shared__ __attribute__((aligned(16))) W buf[kT][kTileWords];
+  __shared__ uint32_t waveCnt[kT][kWaves];
   __shared__ uint32_t red[kWaves];
   const uint32_t b = batchOffset + blockIdx.y;
   const uint32_t n = sizes[b];
   const bool ok = denseOk[b] != 0 && out.size(b) >= n;
-  const uint32_t tile = blockIdx.x;
+  const uint32_t tile0 = blockIdx.x * kT;
   const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  if (tile == 0 && tid == 0) {
+  if (blockIdx.x == 0 && tid == 0) {
     if (outSuccess) outSuccess[b] = ok ? 1 : 0;
     if (outSize) outSize[b] = n;  // fill_in_nonzeros :107-109
   }
-  const uint32_t t0 = tile * kTileWords;
-  if (!ok || t0 >= n) return;
+  if (!ok || tile0 * kTileWords >= n) return;
   gp<const uint8_t> bm = (gp<const uint8_t>)in.start(b) + 16;
-  uint64_t m[kSteps];
-  uint32_t cnt = 0;
+  uint64_t m[kT][kSteps];
+  uint32_t cnt[kT];
 #pragma unroll
-  for (uint32_t j = 0; j < kSteps; ++j) {
-    const uint32_t i0 = t0 + w * (kTileWords / kWaves) + 64 * j;
-    m[j] = i0 < n ? maskToBitmap(*(gp<const uint64_t>)(bm + i0 / 8)) : 0ull;
-    if (i0 < n && n - i0 < 64) m[j] &= (1ull << (n - i0)) - 1;
-    cnt += uint32_t(__popcll(m[j]));
+  for (uint32_t t = 0; t < kT; ++t) {
+    cnt[t] = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < kSteps; ++j) {
+      const uint32_t i0 = (tile0 + t) * kTileWords + w * (kTileWords / kWaves) + 64 * j;
+      m[t][j] = i0 < n ? maskToBitmap(*(gp<const uint64_t>)(bm + i0 / 8)) : 0ull;
+      if (i0 < n && n - i0 < 64) m[t][j] &= (1ull << (n - i0)) - 1;
+      cnt[t] += uint32_t(__popcll(m[t][j]));
+    }
   }
-  // the tile's first list index: the earlier tiles' popcounts (in flight
+  // the first tile's list index: the earlier tiles' popcounts (in flight
   // together with the bitmap loads above)
-  uint32_t pos = tilePrefix(G(tileCounts) + uint64_t(b) * tilesPerElem, tile, red);
-  if (lane == 0) waveCnt[w] = cnt;
+  uint32_t pos = tilePrefix(G(tileCounts) + uint64_t(b) * tilesPerElem, tile0, red);
+  if (lane == 0) {
+#pragma unroll
+    for (uint32_t t = 0; t < kT; ++t) waveCnt[t][w] = cnt[t];
+  }
   __syncthreads();
-  for (uint32_t k = 0; k < w; ++k) pos += waveCnt[k];
   gp<const W> list = (gp<const W>)lists.start(b);
   // x[n-1] is read from idx[n-2] + 1 (fill_in_nonzeros :139-144)
   const bool gap = n >= 2 && ((bm[(n - 2) / 8] >> (7 - (n - 2) % 8)) & 1) == 0;
 #pragma unroll
-  for (uint32_t j = 0; j < kSteps; ++j) {
-    const uint32_t q = w * (kTileWords / kWaves) + 64 * j + lane;
-    const uint32_t i = t0 + q;
-    const bool f = (m[j] >> lane) & 1;
-    uint32_t src = pos + mbcnt(m[j]);
-    if (i + 1 == n && gap) src += 1;
-    buf[q] = f ? list[src] : W(0);
-    pos += uint32_t(__popcll(m[j]));
+  for (uint32_t t = 0; t < kT; ++t) {
+    uint32_t p = pos;
+    for (uint32_t k = 0; k < w; ++k) p += waveCnt[t][k];
+#pragma unroll
+    for (uint32_t j = 0; j < kSteps; ++j) {
+      const uint32_t q = w * (kTileWords / kWaves) + 64 * j + lane;
+      const uint32_t i = (tile0 + t) * kTileWords + q;
+      const bool f = (m[t][j] >> lane) & 1;
+      uint32_t src = p + mbcnt(m[t][j]);
+      if (i + 1 == n && gap) src += 1;
+      buf[t][q] = f ? list[src] : W(0);
+      p += uint32_t(__popcll(m[t][j]));
+    }
+    for (uint32_t k = 0; k < kWaves; ++k) pos += waveCnt[t][k];
   }
   __syncthreads();
   gp<W> y = (gp<W>)out.start(b);
-  const uint32_t tileN = min(kTileWords, n - t0);
-  if (kVec) {
-    constexpr uint32_t kWPV = 16 / sizeof(W);
 #pragma unroll
-    for (uint32_t v = 0; v < kVecs; ++v) {
-      const uint32_t wi = (v * kThreads + tid) * kWPV;
-      if (wi + kWPV <= tileN) {
-        const u32x4 val = *(lp<const u32x4>)&buf[wi];
-        // streaming: nothing here re-reads the output
-        st16nt((gp<uint4>)(y + t0 + wi), make_uint4(val.x, val.y, val.z, val.w));
-      } else {
-        for (uint32_t k = wi; k < tileN && k < wi + kWPV; ++k) y[t0 + k] = buf[k];
+  for (uint32_t t = 0; t < kT; ++t) {
+    const uint32_t t0 = (tile0 + t) * kTileWords;
+    if (t0 >= n) break;
+    const uint32_t tileN = min(kTileWords, n - t0);
+    if (kVec) {
+      constexpr uint32_t kWPV = 16 / sizeof(W);
+#pragma unroll
+      for (uint32_t v = 0; v < kVecs; ++v) {
+        const uint32_t wi = (v * kThreads + tid) * kWPV;
+        if (wi + kWPV <= tileN) {
+          const u32x4 val = *(lp<const u32x4>)&buf[t][wi];
+          // streaming: nothing here re-reads the output
+          st16nt((gp<uint4>)(y + t0 + wi), make_uint4(val.x, val.y, val.z, val.w));
+        } else {
+          for (uint32_t k = wi; k < tileN && k < wi + kWPV; ++k) y[t0 + k] = buf[t][k];
+        }
       }
+    } else {
+      for (uint32_t i = tid; i < tileN; i += kThreads) y[t0 + i] = buf[t][i];
     }
-  } else {
-    for (uint32_t i = tid; i < tileN; i += kThreads) y[t0 + i] = buf[i];
   }
 }
 
@@ -404,6 +439,16 @@ void sparseCompressT(StackDeviceMemory& res, const FloatCompressConfig& config, 
   const uint32_t R = std::min(tiles, kReduceRows);
   auto hist = res.alloc<uint32_t>(s, countHist ? size_t(kSegs) * nb * R * kNumSymbols : 1);
   if (countHist) zeroAsync(hist.data(), size_t(kSegs) * nb * R * kNumSymbols * 4, s);
+  auto table = res.alloc<uint4>(s, countHist ? size_t(kSegs) * nb * kNumSymbols : 1);
+  auto pdf = res.alloc<uint16_t>(s, countHist ? size_t(kSegs) * nb * kNumSymbols : 1);
+  NormArgs na{};
+  na.in = in;
+  na.hist = hist.data();
+  na.rows = R;
+  na.pb = config.ansConfig.probBits;
+  na.table = table.data();
+  na.pdf = pdf.data();
+  na.totalFromHist = true;  // the list length is written by this same launch
   for (uint32_t y0 = 0; y0 < nb; y0 += kMaxGridY) {
     const uint32_t ny = std::min(kMaxGridY, nb - y0);
     prof::Scope p("sparse", s);
@@ -419,11 +464,13 @@ void sparseCompressT(StackDeviceMemory& res, const FloatCompressConfig& config, 
       else launch(std::false_type{}, std::false_type{});
     }
     HIP_LAUNCH_CHECK();
-    k_sparseGather<FT><<<dim3(tiles, ny), kThreads, 0, s>>>(in, y0, tiles, tileCounts.data(), listLen.data(),
-                                                             staging.data(), lists);
+    k_sparseGather<FT><<<dim3(tiles + (countHist ? 1 : 0), ny), kThreads, 0, s>>>(
+        in, y0, tiles, tileCounts.data(), listLen.data(), staging.data(), lists, na);
     HIP_LAUNCH_CHECK();
   }
-  const PartialHist pre{hist.data(), R};
+  PartialHist pre{hist.data(), R};
+  pre.table = table.data();
+  pre.pdf = pdf.data();
   floatCompressDescs(res, config, nb, lists, maxN, denseOut, outSize_dev, s, nullptr, true,
                      countHist ? &pre : nullptr, sparseN);
 }
@@ -475,14 +522,15 @@ FloatDecompressStatus sparseDecompressT(StackDeviceMemory& res,
   for (uint32_t y0 = 0; y0 < nb; y0 += kMaxGridY) {
     const uint32_t ny = std::min(kMaxGridY, nb - y0);
     prof::Scope p("sparse", s);
+    // (fp64: 32 KB per tile of LDS; one tile per workgroup)
+    constexpr uint32_t kT = sizeof(WordOf<FT>) <= 4 ? kExpandTiles : 1;
+    const dim3 g(divUp(tiles, kT), ny);
     if (outAligned16) {
-      k_sparseExpand<FT, true><<<dim3(tiles, ny), kThreads, 0, s>>>(
-          in, out, y0, tiles, sizes.data(), tileCounts.data(), lists, denseOk.data(), outSuccess_dev,
-          outSize_dev);
+      k_sparseExpand<FT, true, kT><<<g, kThreads, 0, s>>>(in, out, y0, tiles, sizes.data(), tileCounts.data(), lists,
+                                                           denseOk.data(), outSuccess_dev, outSize_dev);
     } else {
-      k_sparseExpand<FT, false><<<dim3(tiles, ny), kThreads, 0, s>>>(
-          in, out, y0, tiles, sizes.data(), tileCounts.data(), lists, denseOk.data(), outSuccess_dev,
-          outSize_dev);
+      k_sparseExpand<FT, false, kT><<<g, kThreads, 0, s>>>(in, out, y0, tiles, sizes.data(), tileCounts.data(), lists,
+                                                            denseOk.data(), outSuccess_dev, outSize_dev);
     }
     HIP_LAUNCH_CHECK();
   }
