@@ -183,6 +183,7 @@ PLAINALL = PLAINPART + [
                        __HIP_MEMORY_SCOPE_AGENT);""", """    __hip_atomic_store(G(ka.elog) + uint64_t(T) * ka.maxR + r, tag | min(e, ka.nb), __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_WORKGROUP);""")]
 VARS = {
+    "bpw4": [("codec.hip", "      const uint32_t bpw = 8;", "      const uint32_t bpw = 4;")],
     "kt2": [("sparse.hip", "constexpr uint32_t kExpandTiles = 1;", "constexpr uint32_t kExpandTiles = 2;")],
     "plainall": PLAINALL,
     "plainpart": PLAINPART,
