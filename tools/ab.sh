@@ -14,6 +14,6 @@ for L in "$@"; do
 import json
 for l in open('gpurun_out/ab_$T.log'):
     if l.startswith('{'):
-        d = json.loads(l); print('$T', d['value'], d['ms_per_step'], d['kernels'])"
+        d = json.loads(l); h = d.get('decode_hbm') or {}; print('$T', d['value'], d['ms_per_step'], d['kernels'], 'dec warm/cold', h.get('decode_warm_ms'), h.get('decode_cold_ms'))"
 done
 cp /tmp/ab_default.so "$LIB"
