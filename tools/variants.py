@@ -184,6 +184,11 @@ PLAINALL = PLAINPART + [
                        __HIP_MEMORY_SCOPE_WORKGROUP);""")]
 VARS = {
     "bpw4": [("codec.hip", "      const uint32_t bpw = 8;", "      const uint32_t bpw = 4;")],
+    # sparse count diagnostics (timing only: archives wrong)
+    "sp_noga": [(SP, "      if (sum)\n        __hip_atomic_fetch_add(G(histRows)", "      if (sum == 0xFFFFFFFFu)\n        __hip_atomic_fetch_add(G(histRows)")],
+    "sp_nolds": [(SP, "      if (i + 1 == n && gap) count(W(0));\n      if (v != W(0)) count(v);", "      if (v == W(0x12345u)) count(v);")],
+    "sp_nostage": [(SP, "    if (i + 1 == n && gap) {\n      st[dst] = W(0);\n      if (v != W(0)) st[dst + 1] = v;\n    } else if (v != W(0)) {\n      st[dst] = v;\n    }", "    if (v == W(0x12345u)) st[dst] = v;")],
+    "sp_r256": [(SP, "  const uint32_t R = std::min(tiles, kReduceRows);", "  const uint32_t R = std::min(tiles, 4 * kReduceRows);")],
     "kt2": [("sparse.hip", "constexpr uint32_t kExpandTiles = 1;", "constexpr uint32_t kExpandTiles = 2;")],
     "plainall": PLAINALL,
     "plainpart": PLAINPART,
