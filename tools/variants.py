@@ -189,6 +189,8 @@ VARS = {
     "sp_nolds": [(SP, "      if (i + 1 == n && gap) count(W(0));\n      if (v != W(0)) count(v);", "      if (v == W(0x12345u)) count(v);")],
     "sp_nostage": [(SP, "    if (i + 1 == n && gap) {\n      st[dst] = W(0);\n      if (v != W(0)) st[dst + 1] = v;\n    } else if (v != W(0)) {\n      st[dst] = v;\n    }", "    if (v == W(0x12345u)) st[dst] = v;")],
     "sp_r256": [(SP, "  const uint32_t R = std::min(tiles, kReduceRows);", "  const uint32_t R = std::min(tiles, 4 * kReduceRows);")],
+    "slp0": [(P, "        if (spins) __builtin_amdgcn_s_sleep(2);", "")],
+    "slp1": [(P, "        if (spins) __builtin_amdgcn_s_sleep(2);", "        if (spins) __builtin_amdgcn_s_sleep(1);")],
     "kt2": [("sparse.hip", "constexpr uint32_t kExpandTiles = 1;", "constexpr uint32_t kExpandTiles = 2;")],
     "plainall": PLAINALL,
     "plainpart": PLAINPART,
