@@ -191,6 +191,7 @@ VARS = {
     "sp_r256": [(SP, "  const uint32_t R = std::min(tiles, kReduceRows);", "  const uint32_t R = std::min(tiles, 4 * kReduceRows);")],
     "slp0": [(P, "        if (spins) __builtin_amdgcn_s_sleep(2);", "")],
     "slp1": [(P, "        if (spins) __builtin_amdgcn_s_sleep(2);", "        if (spins) __builtin_amdgcn_s_sleep(1);")],
+    "pcd3": [(P, "  constexpr int D = 2;", "  constexpr int D = 3;")],
     "kt2": [("sparse.hip", "constexpr uint32_t kExpandTiles = 1;", "constexpr uint32_t kExpandTiles = 2;")],
     "plainall": PLAINALL,
     "plainpart": PLAINPART,
