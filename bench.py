@@ -425,7 +425,7 @@ def _extras(dev, pb, reps=3):
 
     def record(name, U, C_bytes, tc, td, exact, **kw):
         out.append({"config": name, "uncompressed_bytes": U, "ratio": round(C_bytes / U, 5),
-                    "compress_ms": round(tc, 3), "decompress_ms": round(td, 3),
+                    "compress_ms": round(tc, 4), "decompress_ms": round(td, 4),
                     "compress_GBps": round(U / tc / 1e6, 1), "decompress_GBps": round(U / td / 1e6, 1),
                     "encode_plus_decode_GBps": round(U / (tc + td) / 1e6, 1),
                     "algorithmic_GBps": round(2 * (U + C_bytes) / (tc + td) / 1e6, 1),
@@ -546,7 +546,223 @@ def _extras(dev, pb, reps=3):
         record(f"c4: {nbs} x 15M fp32, 90 % zeros (sparse bitmap + dense codec)", nbs * 15000000 * 4,
                int(sizes.to(torch.int64).sum()), tc, td, exact, kernels_ms=kern)
         del fs, ys, arch, rows
+    del x, y, ws
+    torch.cuda.empty_cache()
+    out.extend(_extras_small_batches(dev, pb, record, breakdown))
+    out.extend(_extras_batch1_sweep(dev, pb, record, breakdown))
+    out.extend(_extras_reference_grid(dev))
+    out.append(_extras_c5_g1(dev, pb))
     return out
+
+
+def _bf16_trunc(nb, words, seed, dev):
+    """[nb, words] N(0,1) fp32 truncated to bf16, generated in
+    row chunks of at most 2^28 words (fp32 temporaries)."""
+    import torch
+
+    x = torch.empty([nb, words], dtype=torch.bfloat16, device=dev)
+    g = torch.Generator(device=dev).manual_seed(seed)
+    flat = x.view(-1)
+    step = 1 << 28
+    for i in range(0, flat.numel(), step):
+        m = min(step, flat.numel() - i)
+        f = torch.randn(m, generator=g, device=dev, dtype=torch.float32)
+        flat[i:i + m] = (f.view(torch.int32) >> 16).to(torch.int16).view(torch.bfloat16)
+        del f
+    return x
+
+
+def _extras_small_batches(dev, pb, record, breakdown):
+    """batches whose single-pass teams were not
+    XCD-aligned before round 5 (1-7 multi-item elements; 33 x 1e6 words,
+    whose teams cannot be aligned within the resident grid), with the
+    compressor's team-barrier fallback count over every timed call (must be
+    0: a fallback means a hand-off that waited out the 200 us budget)."""
+    import torch
+
+    from dietgpu_fork_amd import codec as C
+
+    for nb, words in ((1, 1000000), (1, 524288), (3, 524288), (33, 1000000)):
+        x = _bf16_trunc(nb, words, 17 + nb, dev)
+        ws = C.Workspace(1 << 30, dev)
+        arch, sizes = C.float_compress_stride(x, prob_bits=pb, ws=ws)
+        y, ok, _ = C.float_decompress_stride(arch, words, torch.bfloat16, prob_bits=pb, ws=ws)
+        C.barrier_fallback_count(reset=True)
+        tc = _timed(lambda: C.float_compress_stride(x, prob_bits=pb, ws=ws, out=arch, sizes=sizes), 3,
+                    max_reps=400)
+        fb = C.barrier_fallback_count(reset=True)
+        td = _timed(lambda: C.float_decompress_stride(arch, words, torch.bfloat16, prob_bits=pb, ws=ws, out=y), 3,
+                    max_reps=400)
+        exact = bool((ok == 1).all()) and torch.equal(x.view(torch.int16), y.view(torch.int16))
+        kern = breakdown(lambda: C.float_compress_stride(x, prob_bits=pb, ws=ws, out=arch, sizes=sizes),
+                         lambda: C.float_decompress_stride(arch, words, torch.bfloat16, prob_bits=pb, ws=ws,
+                                                           out=y))
+        record(f"small batch {nb} x {words} bf16 N(0,1) (floatCompress stride; single-pass team layout)",
+               x.numel() * 2, int(sizes.to(torch.int64).sum()), tc, td, exact, kernels_ms=kern,
+               barrier_fallbacks=fb)
+        del x, y, arch, ws
+    torch.cuda.empty_cache()
+    return []
+
+
+def _extras_batch1_sweep(dev, pb, record, breakdown):
+    """The reference's published batch-1 bf16 curve (README.md:112-118, the
+    A100 plot: 1e6 / 16e6 / 128e6 / 1.07e9 words)."""
+    import torch
+
+    from dietgpu_fork_amd import codec as C
+
+    for words in (1000000, 16000000, 128000000, 1070000000):
+        x = _bf16_trunc(1, words, 19, dev)
+        ws = C.Workspace((1 << 30) + 2 * words * 2, dev)
+        arch, sizes = C.float_compress_stride(x, prob_bits=pb, ws=ws)
+        y, ok, _ = C.float_decompress_stride(arch, words, torch.bfloat16, prob_bits=pb, ws=ws)
+        reps = 3 if words > 1e8 else 10
+        tc = _timed(lambda: C.float_compress_stride(x, prob_bits=pb, ws=ws, out=arch, sizes=sizes), reps,
+                    max_reps=400)
+        td = _timed(lambda: C.float_decompress_stride(arch, words, torch.bfloat16, prob_bits=pb, ws=ws, out=y),
+                    reps, max_reps=400)
+        exact = bool((ok == 1).all()) and torch.equal(x.view(torch.int16), y.view(torch.int16))
+        kern = breakdown(lambda: C.float_compress_stride(x, prob_bits=pb, ws=ws, out=arch, sizes=sizes),
+                         lambda: C.float_decompress_stride(arch, words, torch.bfloat16, prob_bits=pb, ws=ws,
+                                                           out=y))
+        record(f"batch-1 sweep: 1 x {words:.3g} bf16 N(0,1) (README.md:118 A100 curve)", x.numel() * 2,
+               int(sizes.to(torch.int64).sum()), tc, td, exact, kernels_ms=kern)
+        del x, y, arch, ws
+        torch.cuda.empty_cache()
+    return []
+
+
+def _extras_reference_grid(dev):
+    """benchmark.py:151-223, measured as the reference measures it: through
+    torch.ops.dietgpu.compress_data / decompress_data with a 384 MiB temp
+    buffer, float codec and raw-ANS byte codec on bf16 / fp16 / fp32
+    N(0,1) data, non-batched (1 x 128*512*1024) and batched
+    (128 x 512*1024); an event pair around each op call, the first of four
+    runs untimed (benchmark.py:27-90), then the same calls back to back
+    (device throughput without the host's per-call latency)."""
+    import torch
+
+    import dietgpu_fork_amd  # noqa: F401
+
+    res = []
+    tmp = torch.empty([384 << 20], dtype=torch.uint8, device=dev)
+    for as_float in (True, False):
+        for dt in (torch.bfloat16, torch.float16, torch.float32):
+            for shape in ("non-batched [128 * 512 * 1024]", "batched [128, [512 * 1024]]"):
+                g = torch.Generator(device=dev).manual_seed(23)
+                if shape.startswith("non"):
+                    ts = [torch.normal(0, 1.0, [128 * 512 * 1024], generator=g, device=dev).to(dt)]
+                else:
+                    ts = [torch.normal(0, 1.0, [512 * 1024], generator=g, device=dev).to(dt) for _ in range(128)]
+                size_fn = (torch.ops.dietgpu.max_float_compressed_output_size if as_float
+                           else torch.ops.dietgpu.max_any_compressed_output_size)
+                rows, cols = size_fn(ts)
+                comp = torch.empty([rows, cols], dtype=torch.uint8, device=dev)
+                sizes = torch.zeros([len(ts)], dtype=torch.int, device=dev)
+                outs = [torch.empty_like(t) for t in ts]
+                st = torch.empty([len(ts)], dtype=torch.uint8, device=dev)
+                osz = torch.empty([len(ts)], dtype=torch.int32, device=dev)
+                comp_ts = [*comp]
+
+                def fc():
+                    torch.ops.dietgpu.compress_data(as_float, ts, False, tmp, comp, sizes)
+
+                def fd():
+                    torch.ops.dietgpu.decompress_data(as_float, comp_ts, outs, False, tmp, st, osz)
+
+                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                tcs, tds = [], []
+                for i in range(4):
+                    a.record()
+                    fc()
+                    b.record()
+                    torch.cuda.synchronize()
+                    tcs.append(a.elapsed_time(b))
+                    a.record()
+                    fd()
+                    b.record()
+                    torch.cuda.synchronize()
+                    tds.append(a.elapsed_time(b))
+                exact = bool((st == 1).all()) and all(torch.equal(p.view(torch.uint8), q.view(torch.uint8))
+                                                      for p, q in zip(ts, outs))
+                U = sum(t.numel() * t.element_size() for t in ts)
+                Cb = int(sizes.to(torch.int64).sum())
+                tc_ref, td_ref = sum(tcs[1:]) / 3, sum(tds[1:]) / 3
+                tc, td = _timed(fc, 3), _timed(fd, 3)
+                call = 2 * (U + Cb) / ((tc + td) * 1e-3) / 1e9
+                res.append({
+                    "config": f"benchmark.py {'float codec' if as_float else 'raw ANS byte-wise'} "
+                              f"{shape} {str(dt)[6:]} (torch.ops.dietgpu, 384 MiB temp)",
+                    "uncompressed_bytes": U, "ratio": round(Cb / U, 5),
+                    "ref_protocol_compress_ms": round(tc_ref, 4), "ref_protocol_decompress_ms": round(td_ref, 4),
+                    "ref_protocol_compress_GBps": round(U / tc_ref / 1e6, 1),
+                    "ref_protocol_decompress_GBps": round(U / td_ref / 1e6, 1),
+                    "compress_ms": round(tc, 4), "decompress_ms": round(td, 4),
+                    "compress_GBps": round(U / tc / 1e6, 1), "decompress_GBps": round(U / td / 1e6, 1),
+                    "roundtrip_bit_exact": exact,
+                    "roofline": {"bound": "hbm", "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                                 "call_achieved": round(call, 1), "call_frac": round(call / HBM_PEAK_GBPS, 4)}})
+                del ts, outs, comp, comp_ts
+    del tmp
+    torch.cuda.empty_cache()
+    return res
+
+
+def _extras_c5_g1(dev, pb, steps=10):
+    """c5 at G = 1 (BASELINE configs[4]: 8192 x 1 MiB bf16, the whole
+    strong-scaling batch on one GPU): the N = 1 anchor of the scaling curve,
+    same step as the headline (pointer API compress + decompress)."""
+    import torch
+
+    from dietgpu_fork_amd import _native as N
+    from dietgpu_fork_amd import codec as C
+
+    nb, n = 8192, 524288
+    x = _bf16_rows(0, nb, n, dev)
+    L = N.lib()
+    cols = L.dietgpu_get_max_float_compressed_size(2, n)
+    comp = torch.empty([nb, cols], dtype=torch.uint8, device=dev)
+    sizes = torch.empty([nb], dtype=torch.int32, device=dev)
+    out = torch.empty_like(x)
+    ok = torch.empty([nb], dtype=torch.uint8, device=dev)
+    osz = torch.empty([nb], dtype=torch.int32, device=dev)
+    ws = C.Workspace(768 << 20, dev)
+    in_ptrs = N.ptr_array([x.data_ptr() + i * n * 2 for i in range(nb)])
+    in_size = N.u32_array([n] * nb)
+    comp_ptrs = N.ptr_array([comp.data_ptr() + i * cols for i in range(nb)])
+    out_ptrs = N.ptr_array([out.data_ptr() + i * n * 2 for i in range(nb)])
+    caps = N.u32_array([n] * nb)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    C.barrier_fallback_count(reset=True)
+
+    def step():
+        N.check(L.dietgpu_float_compress(ws.h, 2, pb, 0, nb, in_ptrs, in_size, comp_ptrs, sizes.data_ptr(), stream))
+        N.check(L.dietgpu_float_decompress(ws.h, 2, pb, 0, nb, comp_ptrs, out_ptrs, caps, ok.data_ptr(),
+                                           osz.data_ptr(), stream))
+
+    for _ in range(3):
+        step()
+    torch.cuda.synchronize()
+    exact = bool((ok == 1).all()) and torch.equal(out.view(torch.int16), x.view(torch.int16))
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) / steps * 1e3
+    U = nb * n * 2
+    Cb = int(sizes.to(torch.int64).sum())
+    alg = 2 * (U + Cb) / (ms * 1e-3) / 1e9
+    fb = C.barrier_fallback_count(reset=True)
+    r = {"config": "c5 at G = 1: 8192 x 1 MiB bf16 N(0,1), pointer API compress + decompress "
+                   "(BASELINE configs[4], the strong-scaling batch on one GPU)",
+         "uncompressed_bytes": U, "ratio": round(Cb / U, 5), "ms_per_step": round(ms, 3),
+         "GBps": round(U / ms / 1e6, 1), "steps": steps, "roundtrip_bit_exact": exact, "barrier_fallbacks": fb,
+         "roofline": {"bound": "hbm", "peak": HBM_PEAK_GBPS, "unit": "GB/s", "call_achieved": round(alg, 1),
+                      "call_frac": round(alg / HBM_PEAK_GBPS, 4)}}
+    del x, comp, out, ws
+    torch.cuda.empty_cache()
+    return r
 
 
 # profiling family (csrc/profile.h scopes) -> kernel symbol

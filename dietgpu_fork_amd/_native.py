@@ -37,6 +37,7 @@ def _declare(L):
     sig = {
         "dietgpu_last_error": (ctypes.c_char_p, []),
         "dietgpu_device_error_count": (c_u32, [c_int]),
+        "dietgpu_barrier_fallback_count": (c_u32, [c_int]),
         "dietgpu_set_spin_cap": (None, [c_u32]),
         "dietgpu_set_barrier_budget": (None, [c_u32]),
         "dietgpu_set_dispatch_skew": (None, [c_u32]),

@@ -64,6 +64,13 @@ def device_error_count(reset=True):
     return int(N.lib().dietgpu_device_error_count(int(reset)))
 
 
+def barrier_fallback_count(reset=True):
+    """Single-pass compressor team-barrier fallbacks (a workgroup that counted
+    its element from the input after waiting out the barrier budget; the
+    archive is unchanged) since the last reset; synchronises the device."""
+    return int(N.lib().dietgpu_barrier_fallback_count(int(reset)))
+
+
 def set_dispatch_skew(ticks):
     """Test hook: emulate out-of-order workgroup dispatch (0 = off)."""
     N.lib().dietgpu_set_dispatch_skew(int(ticks))

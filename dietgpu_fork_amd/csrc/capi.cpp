@@ -308,6 +308,15 @@ uint32_t dietgpu_device_error_count(int reset) {
   return v;
 }
 
+uint32_t dietgpu_barrier_fallback_count(int reset) {
+  uint32_t v = 0;
+  guarded([&] {
+    v = barrierFallbackCount(reset != 0);
+    return DIETGPU_OK;
+  });
+  return v;
+}
+
 void dietgpu_set_spin_cap(uint32_t polls) { setSpinCap(polls); }
 void dietgpu_set_barrier_budget(uint32_t ticks) { setBarrierBudget(ticks); }
 void dietgpu_set_dispatch_skew(uint32_t ticks) { setDispatchSkew(ticks); }

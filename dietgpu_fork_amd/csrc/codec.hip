@@ -164,9 +164,11 @@ struct DeviceDescs {
 // ---------------------------------------------------------------------------
 // generic drivers
 // ---------------------------------------------------------------------------
-// Device error word: elements the compressor poisoned (a bounded wait ran out,
-// pcompress.h); its outSize is 0.  One per device (code object global).
-__device__ uint32_t g_dgErrors;
+// Device error words (one pair per device, code object global): [0] elements
+// the compressor poisoned (a bounded wait ran out, pcompress.h; their outSize
+// is 0), [1] k_pcompress team-barrier fallbacks (a workgroup that counted its
+// element from the input after the time budget; archives stay exact).
+__device__ uint32_t g_dgErrors[2];
 
 uint32_t* deviceErrorWord() {
   static std::mutex m;
@@ -182,8 +184,8 @@ uint32_t* deviceErrorWord() {
   return static_cast<uint32_t*>(p);
 }
 
-uint32_t deviceErrorCount(bool reset) {
-  uint32_t* p = deviceErrorWord();
+static uint32_t readErrorWord(uint32_t k, bool reset) {
+  uint32_t* p = deviceErrorWord() + k;
   HIP_CHECK(hipDeviceSynchronize());
   uint32_t v = 0;
   HIP_CHECK(hipMemcpy(&v, p, sizeof(v), hipMemcpyDeviceToHost));
@@ -191,12 +193,22 @@ uint32_t deviceErrorCount(bool reset) {
   return v;
 }
 
+uint32_t deviceErrorCount(bool reset) { return readErrorWord(0, reset); }
+uint32_t barrierFallbackCount(bool reset) { return readErrorWord(1, reset); }
+
 // Single-pass compression (k_pcompress, pcompress.h) for single-segment
 // formats without a caller-supplied histogram, elements of at most
 // pc::kMaxTeam items (1 MiB of symbols).  One generation of resident
 // workgroups pulls items off the work queue.
 bool persistentFits(uint32_t maxWords) {
   return divUp(divUp(maxWords, kBlockSize), pc::kBlocksPerItem) <= pc::kMaxTeam;
+}
+
+template <int FT, bool kCk, bool kXcd>
+void launchPersistent(uint32_t grid, hipStream_t s, const DeviceTables* tabs, const BatchDesc& in,
+                      const BatchDesc& out, const PCompArgs& a) {
+  k_pcompress<FT, kCk, kXcd><<<grid, pc::kThreads, 0, s>>>(kernargTable(tabs), in, out, a);
+  HIP_LAUNCH_CHECK();
 }
 
 template <int FT, bool kCk>
@@ -210,16 +222,20 @@ bool compressPersistent(StackDeviceMemory& res, int pb, bool useChecksum, uint32
   const uint64_t items64 = uint64_t(team) * nb;
   DG_CHECK(items64 < (1ull << 30), "batch too large for one compress call");
   const uint32_t items = uint32_t(items64);
-  const uint32_t slots = residentSlots(reinterpret_cast<const void*>(&k_pcompress<FT, kCk>), pc::kThreads, 0);
+  // (both instances have the same resources: one occupancy query)
+  const uint32_t slots = residentSlots(reinterpret_cast<const void*>(&k_pcompress<FT, kCk, true>), pc::kThreads, 0);
   // rounds of whole teams, balanced: R rounds of ceil(nb / R) teams
   const uint32_t maxTeams = std::max(1u, slots / team);
   const uint32_t rounds = divUp(nb, maxTeams);
   uint32_t teamsPerRound = divUp(nb, rounds);
-  bool xcdTeams = false;
-  if (teamsPerRound >= 8 && roundUp(teamsPerRound, 8) <= maxTeams && divUp(nb, roundUp(teamsPerRound, 8)) == rounds) {
-    teamsPerRound = roundUp(teamsPerRound, 8);
-    xcdTeams = true;
-  }
+  // XCD-aligned teams (kXcd, pcompress.h) whenever the teams per round round
+  // up to a multiple of 8 within the resident grid (never more rounds; a
+  // batch of fewer than 8 elements gets idle teams that exit at once), so
+  // the partial histograms stay in one L2.  Otherwise (e.g. 33 elements of
+  // 31 items in 1,024 slots) the team members span XCDs and the partials go
+  // out write-through.
+  const bool xcdTeams = roundUp(teamsPerRound, 8) <= maxTeams;
+  if (xcdTeams) teamsPerRound = roundUp(teamsPerRound, 8);
   const uint32_t grid = teamsPerRound * team;
 
   auto slotMem = res.alloc<uint8_t>(s, size_t(grid) * pc::kBlocksPerItem * kSlotDataBytes);
@@ -260,7 +276,6 @@ bool compressPersistent(StackDeviceMemory& res, int pb, bool useChecksum, uint32
   a.slotSpan = std::max(1u, residentCUs());
   a.err = deviceErrorWord();
   a.slots = slotMem.data();
-  a.teamStart = nullptr;
   a.ckIn = FT != 0 && useChecksum ? ck.data() : nullptr;
   a.outSize = outSize_dev;
   a.sparseN = sparseN;
@@ -268,15 +283,14 @@ bool compressPersistent(StackDeviceMemory& res, int pb, bool useChecksum, uint32
   a.team = team;
   a.nb = nb;
   a.grid = grid;
-  a.xcdTeams = xcdTeams ? 1u : 0u;
   a.epoch = lease.epoch;
   a.spinCap = spinCap();
   a.fallbackTicks = barrierBudgetTicks();
   a.pb = pb;
   a.useChecksum = useChecksum;
   prof::Scope p("compress", s);
-  k_pcompress<FT, kCk><<<grid, pc::kThreads, 0, s>>>(kernargTable(tabs), in, out, a);
-  HIP_LAUNCH_CHECK();
+  if (xcdTeams) launchPersistent<FT, kCk, true>(grid, s, tabs, in, out, a);
+  else launchPersistent<FT, kCk, false>(grid, s, tabs, in, out, a);
   return true;
 }
 
@@ -699,11 +713,20 @@ void ansGetCompressedInfo(StackDeviceMemory& res, const void** in, uint32_t numI
 // ---------------------------------------------------------------------------
 // float codec API
 // ---------------------------------------------------------------------------
+// float/GpuFloatCompress.cu:23-47.  The result is a u32 there too and may
+// exceed INT32_MAX (the reference's published batch-1 sweep compresses
+// 1.07e9 bf16 words, README.md:118: 2.41e9 bytes of capacity); every archive
+// offset is unsigned 32-bit, so anything up to UINT32_MAX is accepted.  The
+// raw section is sized in 64 bits here so that an fp32 / fp64 size past the
+// u32 range is refused instead of wrapping.
 uint32_t getMaxFloatCompressedSize(FloatType ft, uint32_t size) {
   DG_CHECK(ft != FloatType::kUndefined && uint32_t(ft) <= 4, "bad float type");
-  uint64_t base = 32ull + getMaxCompressedSize(size) + floatRawBytes(int(ft), size);
+  const uint64_t n8 = roundUp64(size, 8), n16 = roundUp64(size, 16);
+  const uint64_t raw = ft == FloatType::kFloat32 ? 2 * n8 + n16
+                       : ft == FloatType::kFloat64 ? 4 * roundUp64(size, 4) + 2 * n8 : n16;
+  uint64_t base = 32ull + getMaxCompressedSize(size) + raw;
   if (ft == FloatType::kFloat64) base += getMaxCompressedSize(size);
-  DG_CHECK(base <= uint64_t(INT32_MAX), "input too large: " << size << " float words");
+  DG_CHECK(base <= uint64_t(UINT32_MAX), "input too large: " << size << " float words");
   return uint32_t(base);
 }
 

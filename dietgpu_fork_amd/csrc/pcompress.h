@@ -13,11 +13,11 @@
 // block pair per wave); the items of an element form its team.  The grid is
 // at most one generation of resident workgroups, a whole number of teams of
 // workgroups, and a workgroup team takes one element per round: member x of
-// team T works item x of the team's element.  Team membership keeps each
-// team on one XCD (workgroups w, w + 8, ... share one under the observed
-// round-robin placement), so the team's hand-offs stay in one L2 (speed
-// only, never correctness), and gives the members increasing workgroup
-// indices.  Elements of rounds 0 and 1 are static (r * teams + T); from
+// team T works item x of the team's element.  Team membership (kXcd) keeps
+// each team on one XCD (workgroups w, w + 8, ... share one under the
+// observed round-robin placement), so the team's hand-offs stay in one L2
+// (speed only, never correctness), and gives the members increasing
+// workgroup indices.  Elements of rounds 0 and 1 are static (r * teams + T); from
 // round 2 on, member 0 takes the team's element two rounds ahead with one
 // returning add on a per-call counter and logs it (epoch-tagged) for the
 // other members, so teams that ran fast take more elements.  One add per
@@ -42,12 +42,17 @@
 // a partial histogram word is {epoch << 16 | count}, read with sc1 loads, so
 // its consumer needs no arrival flag (no drain of the producer's stores, no
 // barrier, one memory round trip per hop); the look-back flags carry their
-// value and epoch in one 8 B word.  The partials are stored plain (sc0): the
-// line stays in the XCD's L2, where the team's other members -- the same XCD
-// under round-robin placement -- read it at L2 latency (an sc1 store drops the
-// line and every read goes to the fabric: c2 compress 141.5 -> 138.5 us).  A
-// member placed on another XCD could see a stale line; the team barrier's
-// time budget then counts the element from the input (below), so this is
+// value and epoch in one 8 B word.  Where the host could lay the teams out
+// XCD-aligned (kXcd: every batch whose teams per round round up to a multiple
+// of 8 within the resident grid, small batches padded with idle teams) the
+// partials are stored plain (sc0): the line stays in the XCD's L2, where the
+// team's other members -- the same XCD under round-robin placement -- read it
+// at L2 latency (an sc1 store drops the line and every read goes to the
+// fabric: c2 compress 141.5 -> 138.5 us).  Other grids store them sc1
+// (write-through), which a member on any XCD reads fresh.  Were a member
+// ever placed elsewhere and served a stale line, the team barrier's time
+// budget counts the element from the input (below) and the device's fallback
+// word counts the event (dietgpu_barrier_fallback_count), so placement is
 // speed only.  The flags and the log keep sc1 stores: their waits have no
 // such fallback.
 //
@@ -79,7 +84,6 @@
 #include <utility>
 
 #include "encode.h"
-#include "lookback.h"
 #include "sync_arena.h"
 
 namespace dietgpu {
@@ -113,17 +117,15 @@ struct PCompArgs {
   uint32_t* part;        // [items][256] partial histograms, epoch << 16 | count (sync arena)
   uint32_t* partCk;      // [items] partial byte checksums, epoch << 16 | xor (FT 0 with checksum)
   uint64_t* flags;       // [items] look-back flags (sync arena)
-  uint32_t* err;         // device error word (elements poisoned)
+  uint32_t* err;         // device error words: [0] elements poisoned, [1] team-barrier fallbacks
   uint8_t* slots;        // [grid][8][kSlotDataBytes] spill space of each workgroup
-  const uint32_t* teamStart;  // [nb + 1] first item of each element, or null: uniform teams
   const uint32_t* ckIn;  // float checksum per element (k_checksum) or null
   uint32_t* outSize;
   const uint32_t* sparseN;  // EncTail::sparseN
   uint32_t items;        // total items
-  uint32_t team;         // items per element when uniform
+  uint32_t team;         // items per element
   uint32_t nb;
   uint32_t grid;         // workgroups = items per round (a whole number of teams)
-  uint32_t xcdTeams;     // 1: team members share w % 8 (teams per round % 8 == 0)
   uint64_t* ctr;         // [2] element dequeue counters, this call's at epoch & 1 (sync arena)
   uint64_t* elog;        // [teams][maxR] element of each team's round, epoch << 32 | element (sync arena)
   uint32_t maxR;         // rounds a team may take
@@ -146,20 +148,9 @@ __device__ __forceinline__ PItem itemOf(uint32_t i, const PCompArgs& a, const Ba
   it.i = i;
   it.b = it.x = it.team = it.tb = it.n = it.nBlocks = 0;
   if (i >= a.items) return it;
-  if (a.teamStart == nullptr) {
-    it.b = i / a.team;
-    it.team = a.team;
-    it.tb = it.b * a.team;
-  } else {  // largest b with teamStart[b] <= i (scalar loads)
-    uint32_t lo = 0, hi = a.nb;
-    while (hi - lo > 1) {
-      const uint32_t mid = (lo + hi) >> 1;
-      if (BatchDesc::tableAt(a.teamStart, mid) <= i) lo = mid; else hi = mid;
-    }
-    it.b = lo;
-    it.tb = BatchDesc::tableAt(a.teamStart, lo);
-    it.team = BatchDesc::tableAt(a.teamStart, lo + 1) - it.tb;
-  }
+  it.b = i / a.team;
+  it.team = a.team;
+  it.tb = it.b * a.team;
   it.x = i - it.tb;
   it.n = in.size(it.b);
   it.nBlocks = divUp(it.n, kBlockSize);
@@ -212,7 +203,14 @@ __device__ __forceinline__ uint64_t realtime() {
 // Grid: one generation of resident workgroups (1-D), 256 threads.  Pointer
 // tables may ride in the first (InlineTable) argument (BatchDesc::inl).  4
 // waves per SIMD (<= 128 VGPRs, ~40 KB of LDS per workgroup).
-template <int FT, bool kCk>
+// kXcd: the grid is a whole number of 8-team groups and member x of team
+// T = 8 g + c is workgroup c + 8 (g team + x), so a team's workgroups share
+// blockIdx % 8, i.e. one XCD under round-robin placement (speed only); the
+// partial histograms then go out as plain stores that stay in that L2.
+// Otherwise (teams per round not a multiple of 8 within the resident grid)
+// a team's workgroups are consecutive and spread over the XCDs, and the
+// partials are stored write-through (sc1), which every XCD reads fresh.
+template <int FT, bool kCk, bool kXcd>
 __global__ __launch_bounds__(pc::kThreads) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_pcompress(
     const InlineTable, BatchDesc, BatchDesc, PCompArgs) {
   auto IN = [] { return kernArg<BatchDesc>(kArgIn); };
@@ -293,7 +291,7 @@ __global__ __launch_bounds__(pc::kThreads) __attribute__((amdgpu_waves_per_eu(4,
   // work ahead of the last ones).
   auto teamX = [&](uint32_t& T, uint32_t& X) __attribute__((always_inline)) {
     const PCompArgs ka = A();
-    if (ka.xcdTeams) {  // w = xcd + 8 (group * team + x), team T = group * 8 + xcd
+    if constexpr (kXcd) {  // w = xcd + 8 (group * team + x), team T = group * 8 + xcd
       const uint32_t xcd = blockIdx.x & 7u, q = blockIdx.x >> 3;
       const uint32_t grp = q / ka.team;
       X = q - grp * ka.team;
@@ -513,10 +511,11 @@ __global__ __launch_bounds__(pc::kThreads) __attribute__((amdgpu_waves_per_eu(4,
   // (after a workgroup barrier: every wave's counts and ckS are in).  The
   // data carries its own epoch, so the consumer needs no separate arrival
   // flag: no drain of the stores, no barrier, one memory round trip per hop
-  // (MI355X_MICROARCH.md: a tagged granule).  Plain (sc0) stores keep the
-  // line in this XCD's L2 for the team's sc1 loads (header comment).  The
-  // words live in the persistent epoch-tagged sync arena, never in scratch a
-  // stale value could come from.
+  // (MI355X_MICROARCH.md: a tagged granule).  kXcd: plain (sc0) stores keep
+  // the line in this XCD's L2 for the team's sc1 loads (header comment);
+  // otherwise sc1 (write-through) stores, since members on other XCDs read
+  // from memory.  The words live in the persistent epoch-tagged sync arena,
+  // never in scratch a stale value could come from.
   auto publishHist = [&](const PItem& it) __attribute__((always_inline)) {
     const uint32_t tid = tidNow(), lane = laneNow();
     (void)tid;
@@ -528,8 +527,11 @@ __global__ __launch_bounds__(pc::kThreads) __attribute__((amdgpu_waves_per_eu(4,
       hist[tid * pc::kHistStride + k] = 0;
     }
     const uint32_t tag = A().epoch << 16;
-    __hip_atomic_store(G(A().part) + uint64_t(it.i) * kNumSymbols + tid, tag | cnt, __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_WORKGROUP);
+    if constexpr (kXcd)
+      __hip_atomic_store(G(A().part) + uint64_t(it.i) * kNumSymbols + tid, tag | cnt, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_WORKGROUP);
+    else
+      stSc1(G(A().part) + uint64_t(it.i) * kNumSymbols + tid, tag | cnt);
     if constexpr (kCk) {
       if (tid == 0) stSc1(G(A().partCk) + it.i, tag | (ckS[0] ^ ckS[1] ^ ckS[2] ^ ckS[3]));
     }
@@ -948,6 +950,10 @@ __global__ __launch_bounds__(pc::kThreads) __attribute__((amdgpu_waves_per_eu(4,
         }
         if (fb) {
           fbS = 0;
+          // counted per call (dietgpu_barrier_fallback_count): a nonzero
+          // count on an uncontended chip means a hand-off that never lands
+          if (lane == 0)
+            __hip_atomic_fetch_add(G(A().err) + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           countElementWave(L, c, ckL);
         }
         uint32_t cdf[4];

@@ -541,7 +541,7 @@ FloatDecompressStatus sparseDecompressT(StackDeviceMemory& res,
 
 uint32_t getMaxSparseFloatCompressedSize(FloatType ft, uint32_t size) {
   const uint64_t v = 16ull + roundUp64((uint64_t(size) + 7) / 8, 16) + getMaxFloatCompressedSize(ft, size);
-  DG_CHECK(v <= uint64_t(INT32_MAX), "input too large: " << size << " float words");
+  DG_CHECK(v <= uint64_t(UINT32_MAX), "input too large: " << size << " float words");
   return uint32_t(v);
 }
 

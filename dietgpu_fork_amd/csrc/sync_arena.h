@@ -67,6 +67,11 @@ class SyncLease {
 // the last reset (a team barrier or look-back wait ran out of polls: the
 // element's outSize is 0); synchronises the device.
 uint32_t deviceErrorCount(bool reset);
+// Number of k_pcompress team-barrier fallbacks since the last reset (a
+// workgroup that waited out the barrier budget for its team's partial
+// histograms and counted its element from the input; the archive is exact,
+// the call slower); synchronises the device.
+uint32_t barrierFallbackCount(bool reset);
 
 // Polls allowed for each cross-workgroup wait of the compressor before it
 // gives up and poisons the element (default 1 << 24, about 0.5 s).  0 makes
@@ -81,10 +86,11 @@ uint32_t spinCap();
 void setBarrierBudget(uint32_t ticks);
 uint32_t barrierBudgetTicks();
 
-// Test hook: workgroups of the compressors (k_pcompress, k_encode) wait
+// Test hook: workgroups of the fused three-kernel compressor (k_encode) wait
 // (63 - g % 64) * ticks at their start (skewDelay, device.h), so they start in
 // about reverse index order within every 64: the look-backs then wait on
-// late-starting lower workgroups.  0 (default) is off.
+// late-starting lower workgroups.  0 (default) is off.  (k_pcompress carries
+// no hook; the test-only variant tools/variants.py pskew adds one.)
 void setDispatchSkew(uint32_t ticks);
 uint32_t dispatchSkew();
 

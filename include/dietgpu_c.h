@@ -180,6 +180,13 @@ void dietgpu_profile_reset(void);
  * dietgpu_device_error_count synchronises the current device and returns the
  * count since the last reset (reset != 0 clears it). */
 uint32_t dietgpu_device_error_count(int reset);
+/* Number of single-pass compressor team-barrier fallbacks since the last
+ * reset (reset != 0 clears it): a workgroup that waited out the barrier
+ * budget (dietgpu_set_barrier_budget) for its team's partial histograms and
+ * counted its element from the input instead.  Archives are unchanged; a
+ * nonzero count without a competing kernel or a forced budget means a slow
+ * hand-off.  Synchronises the current device. */
+uint32_t dietgpu_barrier_fallback_count(int reset);
 /* Test hook: polls each such wait may make before it gives up (default
  * 1 << 24).  0 makes every wait that would have to wait fail at once, which
  * forces the error path deterministically for elements of more than one
@@ -191,10 +198,11 @@ void dietgpu_set_spin_cap(uint32_t polls);
  * fallback keeps the compressor live when other kernels hold CUs; 0 forces
  * it for every team wait (archives are unchanged). */
 void dietgpu_set_barrier_budget(uint32_t ticks);
-/* Test hook: every compressor workgroup (k_pcompress, and k_encode on the
- * fused three-kernel path) waits (63 - g % 64) * ticks (100 MHz) before it
- * takes its start ticket, so tickets go out in about reverse launch order:
- * out-of-order dispatch, emulated.  Archives are unchanged; 0 = off. */
+/* Test hook: every k_encode workgroup of the fused three-kernel path waits
+ * (63 - g % 64) * ticks (100 MHz) at its start, so the workgroups start
+ * publishing in about reverse index order within every 64 (late publication
+ * by dispatched lower workgroups; the single-pass k_pcompress carries no
+ * hook, see tools/variants.py pskew).  Archives are unchanged; 0 = off. */
 void dietgpu_set_dispatch_skew(uint32_t ticks);
 /* Test hook: enqueue on `stream` a kernel of `workgroups` 256-thread
  * workgroups that each hold `lds_bytes` of LDS for `micros` microseconds

@@ -133,7 +133,14 @@ def test_oversize_requests_raise():
     with pytest.raises(DietGpuError):
         C.max_compressed_size(0xFFFFFFFF)
     with pytest.raises(DietGpuError):
-        C.max_float_compressed_size(3, 1_000_000_000)
+        C.max_float_compressed_size(3, 1_100_000_000)  # 4.67e9 bytes
+    with pytest.raises(DietGpuError):
+        C.max_float_compressed_size(4, 1_000_000_000)
+    # the reference's largest published batch-1 point (README.md:118): the
+    # bound exceeds INT32_MAX but is a valid u32, as in
+    # float/GpuFloatCompress.cu:23-47
+    n = 1_070_000_000
+    assert C.max_float_compressed_size(2, n) == 32 + C.max_compressed_size(n) + (n + 15) // 16 * 16
     with pytest.raises(RuntimeError):
         torch.ops.dietgpu.max_any_compressed_size(4_000_000_000)
     assert C.max_float_compressed_size(2, 524288) == 1737280

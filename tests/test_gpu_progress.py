@@ -108,11 +108,20 @@ def test_compress_beside_occupying_kernel(C, ws):
 
 @pytest.mark.parametrize("shape", ["c2", "c3"])
 def test_out_of_order_dispatch(C, ws, shape):
-    """Workgroups start in about REVERSE index order (test hook: each waits
-    (63 - g % 64) x 1 us first), so the look-backs (k_pcompress's team
-    look-back and log read; k_encode's fused look-back on the c3 path) wait
-    on lower workgroups that start up to 63 us late: archives
-    oracle-identical, nothing abandoned (no wait runs out of polls)."""
+    """Workgroups start in about REVERSE index order within every 64 (each
+    waits (63 - g % 64) x 1 us first), so the look-backs wait on lower
+    workgroups that start up to 63 us late: archives oracle-identical,
+    nothing abandoned (no wait runs out of polls).
+
+    What is covered: late PUBLICATION by lower workgroups, which have been
+    dispatched (the delay runs after dispatch); a lower workgroup that is
+    never dispatched cannot be emulated from software.  c3: k_encode's fused
+    look-back, through the product's skew hook (dietgpu_set_dispatch_skew).
+    c2: k_pcompress carries no hook, so with the
+    product library this leg runs unskewed; tools/skew_check.sh runs it
+    against the test-only variant library tools/ablibs/pskew.so
+    (tools/variants.py pskew), whose k_pcompress starts skewed the same way
+    (team look-back, element-log read, team barrier)."""
     C.device_error_count(reset=True)
     try:
         C.set_dispatch_skew(100)

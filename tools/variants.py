@@ -182,7 +182,16 @@ PLAINALL = PLAINPART + [
     (P, """    __hip_atomic_store(G(ka.elog) + uint64_t(T) * ka.maxR + r, tag | min(e, ka.nb), __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);""", """    __hip_atomic_store(G(ka.elog) + uint64_t(T) * ka.maxR + r, tag | min(e, ka.nb), __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_WORKGROUP);""")]
+# test-only (VERDICT r4 item 2): k_pcompress workgroups start in about
+# reverse index order within every 64 (skewDelay, 1 us steps), so its
+# look-back and element-log waits meet late-starting lower workgroups; run
+# by tools/skew_check.sh against tests/test_gpu_progress.py.  The product
+# kernel carries no hook (a one-line hook tipped its register allocation,
+# DESIGN.md section 7).
+PSKEW = [(P, "  __syncthreads();  // histogram zeroed\n",
+          "  if (tid == 0) skewDelay(100);\n  __syncthreads();  // histogram zeroed\n")]
 VARS = {
+    "pskew": PSKEW,
     "bpw4": [("codec.hip", "      const uint32_t bpw = 8;", "      const uint32_t bpw = 4;")],
     # sparse count diagnostics (timing only: archives wrong)
     "sp_noga": [(SP, "      if (sum)\n        __hip_atomic_fetch_add(G(histRows)", "      if (sum == 0xFFFFFFFFu)\n        __hip_atomic_fetch_add(G(histRows)")],
