@@ -89,9 +89,11 @@ def test_bytes_non_xcd_teams_no_fallback(C, ws, ck):
 
 
 def test_fallback_counter_counts(C, ws):
-    """Budget 0 forces the fallback on every multi-member team wait: the
-    counter must see them (and the archives stay the oracle's)."""
-    words, x = _bf16_batch(3, 524288, seed0=77)
+    """Budget 0 forces the fallback wherever a team member's partial was not
+    in at the first look -- always for teams of more than 16 items (each wave
+    loads only its first four members' partials before the window's barrier):
+    the counter must see them, and the archives stay the oracle's."""
+    words, x = _bf16_batch(3, 1000000, seed0=77)
     C.barrier_fallback_count(reset=True)
     try:
         C.set_barrier_budget(0)
