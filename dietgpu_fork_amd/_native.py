@@ -86,7 +86,8 @@ def _declare(L):
                                           ctypes.POINTER(ctypes.c_uint64)]),
     }
     # test hooks absent from older builds (same-box A/B of earlier libraries)
-    optional = {"dietgpu_set_barrier_budget", "dietgpu_set_dispatch_skew", "dietgpu_test_occupy", "dietgpu_test_histogram"}
+    optional = {"dietgpu_set_barrier_budget", "dietgpu_set_dispatch_skew", "dietgpu_test_occupy", "dietgpu_test_histogram",
+                "dietgpu_barrier_fallback_count"}
     for name, (res, args) in sig.items():
         if name in optional and not hasattr(L, name):
             continue
