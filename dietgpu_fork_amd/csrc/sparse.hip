@@ -250,7 +250,7 @@ __device__ __forceinline__ uint32_t tilePrefix(gp<const uint32_t> counts, uint32
 // (c4 1 x 15M fp32 compress -6 us).
 template <int FT>
 __global__ __launch_bounds__(kThreads) void k_sparseGather(BatchDesc in, uint32_t batchOffset,
-                                                           uint32_t tilesPerElem,
+                                                           uint32_t numInBatch, uint32_t tilesPerElem,
                                                            const uint32_t* __restrict__ tileCounts,
                                                            uint32_t* __restrict__ listLen,
                                                            const WordOf<FT>* __restrict__ staging,
@@ -263,7 +263,7 @@ __global__ __launch_bounds__(kThreads) void k_sparseGather(BatchDesc in, uint32_
     __shared__ __attribute__((aligned(16))) uint32_t keys[kNumSymbols];
     __shared__ u32x4 red4[kThreads];
     for (int sg = 0; sg < FloatTraits<FT>::kSegs; ++sg) {
-      normalizeElement(na, batchOffset + gridDim.y, b, sg, keys, red, red4);  // (used with nb == 1)
+      normalizeElement(na, numInBatch, b, sg, keys, red, red4);
       __syncthreads();
     }
     return;
@@ -465,7 +465,7 @@ void sparseCompressT(StackDeviceMemory& res, const FloatCompressConfig& config, 
     }
     HIP_LAUNCH_CHECK();
     k_sparseGather<FT><<<dim3(tiles + (countHist ? 1 : 0), ny), kThreads, 0, s>>>(
-        in, y0, tiles, tileCounts.data(), listLen.data(), staging.data(), lists, na);
+        in, y0, nb, tiles, tileCounts.data(), listLen.data(), staging.data(), lists, na);
     HIP_LAUNCH_CHECK();
   }
   PartialHist pre{hist.data(), R};

@@ -1,0 +1,113 @@
+"""The compressor's persistent sync arena (csrc/sync_arena.{h,cpp}): the
+single-pass k_pcompress and the fused three-kernel k_encode keep their
+look-back flags, epoch-tagged, in the SAME per-stream region (kSyncFlags), and
+neither zeroes it before a call.  A stale flag of one path must never be read
+as current by the other, across alternating calls on one stream and across
+the 16-bit epoch's wrap-around.  Outputs are sentinel-filled
+before every call, so a byte the compressor failed to write shows; every
+archive must equal the oracle's (the reference writes one archive per element
+whatever the path, ans/GpuANSEncode.cuh:670-845)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as O
+from tests.util import float_words
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+SENTINEL = 0xAB
+
+
+@pytest.fixture(scope="module")
+def env():
+    import dietgpu_fork_amd  # noqa: F401
+    from dietgpu_fork_amd import _native as N
+    from dietgpu_fork_amd import codec as C
+
+    return N, C
+
+
+class Batch:
+    """bf16 elements in one device buffer; `aligned` False offsets every
+    element by one word (not 16 B-aligned: the fused three-kernel path)."""
+
+    def __init__(self, N, sizes, seed, aligned):
+        self.N = N
+        self.words = [float_words(2, n, seed=seed + i) for i, n in enumerate(sizes)]
+        stride = max(sizes) + 64
+        host = np.zeros(len(sizes) * stride, dtype=np.uint16)
+        self.offs = [i * stride + (0 if aligned else 1) for i in range(len(sizes))]
+        for o, w in zip(self.offs, self.words):
+            host[o:o + w.size] = w
+        self.x = torch.from_numpy(host.view(np.int16)).to(DEV)
+        self.cols = N.lib().dietgpu_get_max_float_compressed_size(2, max(sizes))
+        self.out = torch.empty([len(sizes), self.cols], dtype=torch.uint8, device=DEV)
+        self.sizes = torch.empty([len(sizes)], dtype=torch.int32, device=DEV)
+        self.in_ptrs = N.ptr_array([self.x.data_ptr() + 2 * o for o in self.offs])
+        self.in_size = N.u32_array(sizes)
+        self.out_ptrs = N.ptr_array([self.out.data_ptr() + i * self.cols for i in range(len(sizes))])
+
+    def compress(self, ws, stream, fill=True):
+        if fill:
+            self.out.fill_(SENTINEL)
+        self.N.check(self.N.lib().dietgpu_float_compress(ws.h, 2, 10, 0, len(self.words), self.in_ptrs,
+                                                         self.in_size, self.out_ptrs, self.sizes.data_ptr(),
+                                                         stream.cuda_stream))
+
+    def check(self):
+        sizes = self.sizes.cpu().tolist()
+        host = self.out.cpu().numpy()
+        for i, w in enumerate(self.words):
+            ref = O.float_compress(w, 2)
+            assert sizes[i] == ref.size, (i, sizes[i], ref.size)
+            np.testing.assert_array_equal(host[i, : ref.size], ref, err_msg=f"element {i}")
+
+
+def test_alternating_paths_one_stream(env):
+    """Single-pass and fused three-kernel calls back to back on one stream,
+    the same shapes (so the flag words of one land on the other's)."""
+    N, C = env
+    ws = C.Workspace(256 << 20)
+    s = torch.cuda.Stream()
+    sizes = [300000, 524288, 70001, 4097, 200000]
+    a = Batch(N, sizes, seed=11, aligned=True)
+    u = Batch(N, sizes, seed=11, aligned=False)
+    C.device_error_count(reset=True)
+    with torch.cuda.stream(s):
+        for k in range(8):
+            b = a if k % 2 == 0 else u
+            b.compress(ws, s)
+            s.synchronize()
+            b.check()
+    assert C.device_error_count(reset=True) == 0
+
+
+def test_epoch_wraparound(env):
+    """More than 2^16 calls on a fresh stream (the arena's 16-bit epoch
+    wraps and the arena is re-zeroed), alternating the two paths; archives
+    checked before, around and after the wrap."""
+    N, C = env
+    ws = C.Workspace(64 << 20)
+    s = torch.cuda.Stream()
+    sizes = [70000, 40000]  # 3 and 2 single-pass items: look-back and partials
+    a = Batch(N, sizes, seed=21, aligned=True)
+    u = Batch(N, sizes, seed=21, aligned=False)
+    C.device_error_count(reset=True)
+    C.barrier_fallback_count(reset=True)
+    total = (1 << 16) + 40
+    checkpoints = {0, 1, 2, 3, 1000, (1 << 16) - 3, (1 << 16) - 2, (1 << 16) - 1, 1 << 16, (1 << 16) + 1,
+                   (1 << 16) + 2, total - 2, total - 1}
+    with torch.cuda.stream(s):
+        for k in range(total):
+            b = a if k % 2 == 0 else u
+            if k in checkpoints:
+                b.compress(ws, s)
+                s.synchronize()
+                b.check()
+            else:
+                b.compress(ws, s, fill=False)
+    s.synchronize()
+    assert C.device_error_count(reset=True) == 0
+    assert C.barrier_fallback_count(reset=True) == 0

@@ -6,6 +6,7 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 LIB=dietgpu_fork_amd/_lib/libdietgpu_amd.so
 cp "$LIB" /tmp/ab_default.so
+trap 'cp /tmp/ab_default.so "$LIB"' EXIT
 for L in "$@"; do
   T=$(basename "$L" .so)
   if [ "$L" = default ]; then cp /tmp/ab_default.so "$LIB"; else cp "$L" "$LIB"; fi

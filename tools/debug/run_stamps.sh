@@ -4,7 +4,6 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 LIB=dietgpu_fork_amd/_lib/libdietgpu_amd.so
 cp "$LIB" /tmp/stamps_default.so
+trap 'cp /tmp/stamps_default.so "$LIB"' EXIT
 cp "$1" "$LIB"
-timeout -k 10 120 python3 -u "$2"; rc=$?
-cp /tmp/stamps_default.so "$LIB"
-exit $rc
+timeout -k 10 120 python3 -u "$2"

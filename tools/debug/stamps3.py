@@ -18,7 +18,7 @@ from dietgpu_fork_amd import codec as C  # noqa: E402
 L = N.lib()
 L.dietgpu_debug_stamps.restype = ctypes.c_void_p
 hip = ctypes.CDLL("libamdhip64.so")
-nb, n = 256, 524288
+nb, n = int(os.environ.get("NB", 256)), int(os.environ.get("NW", 524288))
 g = torch.Generator(device="cuda").manual_seed(1000)
 x = (torch.randn(nb, n, generator=g, device="cuda").view(torch.int32) >> 16).to(torch.int16).view(torch.bfloat16)
 ws = C.Workspace(768 << 20)

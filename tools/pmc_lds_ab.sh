@@ -6,6 +6,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 LIB=dietgpu_fork_amd/_lib/libdietgpu_amd.so
 cp "$LIB" /tmp/pl_default.so
+trap 'cp /tmp/pl_default.so "$LIB"' EXIT
 for L in "$@"; do
   T=$(basename "$L" .so)
   cp "$L" "$LIB"

@@ -5,6 +5,7 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 LIB=dietgpu_fork_amd/_lib/libdietgpu_amd.so
 cp "$LIB" /tmp/vc_default.so
+trap 'cp /tmp/vc_default.so "$LIB"' EXIT
 rc=0
 for L in "$@"; do
   T=$(basename "$L" .so)
