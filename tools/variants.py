@@ -192,6 +192,20 @@ PSKEW = [(P, "  __syncthreads();  // histogram zeroed\n",
           "  if (tid == 0) skewDelay(100);\n  __syncthreads();  // histogram zeroed\n")]
 VARS = {
     "pskew": PSKEW,
+    # a single-read c3 (4 MiB byte elements, teams of
+    # 128 items) through k_pcompress, measured instead of extrapolated
+    # (timing and archives only; checksummed byte archives would need the
+    # per-member checksum gather widened past 64 lanes)
+    # round 5: one segment of loads in flight (a shallower memory queue for
+    # the hand-off window's loads, which queue behind the CU's streaming)
+    "pcd1": [(P, "  constexpr int D = 2;", "  constexpr int D = 1;")],
+    # round 5: the quotient's shift operand read from byte 3 of the table
+    # entry by SDWA (one VALU per encode step fewer)
+    "sdwa": [("encode.h", "  const uint32_t q = __umulhi(x, e.y) >> (e.w >> 24);",
+              """  uint32_t q;
+  asm("v_lshrrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_3 src1_sel:DWORD"
+      : "=v"(q) : "v"(e.w), "v"(__umulhi(x, e.y)));""")],
+    "pc128": [(P, "constexpr uint32_t kMaxTeam = 32;", "constexpr uint32_t kMaxTeam = 128;")],
     "bpw4": [("codec.hip", "      const uint32_t bpw = 8;", "      const uint32_t bpw = 4;")],
     # sparse count diagnostics (timing only: archives wrong)
     "sp_noga": [(SP, "      if (sum)\n        __hip_atomic_fetch_add(G(histRows)", "      if (sum == 0xFFFFFFFFu)\n        __hip_atomic_fetch_add(G(histRows)")],
