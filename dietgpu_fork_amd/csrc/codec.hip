@@ -314,6 +314,7 @@ void encodeBatchDevice(StackDeviceMemory& res, int pb, bool useChecksum, uint32_
   const uint32_t chunks = preHist ? std::max(1u, pre->nRows) : std::max(1u, divUp(maxSize, chunkWords));
   const bool runHist = !preHist && (!userHist || useChecksum);
   const bool rawCk = FT == 0 && useChecksum;
+  const uint32_t nW = std::max(1u, divUp(MB, EncCfg<FT>::kBlocksPerWG));
   if constexpr (kFused) {
     if (!userHist && inAligned16) {
       const bool done = rawCk ? compressPersistent<FT, FT == 0>(res, pb, useChecksum, nb, inArg,
@@ -327,12 +328,22 @@ void encodeBatchDevice(StackDeviceMemory& res, int pb, bool useChecksum, uint32_
   DeviceDescs dd(res, s, tabs);
   const BatchDesc in = dd.map(inArg), out = dd.map(outArg);
 
-  auto partHist = res.alloc<uint32_t>(s, runHist ? size_t(kSegs) * nb * chunks * kNumSymbols : 1);
+  // Prologue normalisation (k_encode<.., kPro>, encode.h proNormalize):
+  // when the encode grid is at most two generations of resident workgroups,
+  // k_hist accumulates kProRows rows per (segment, element) with atomics (in
+  // the sync arena) and every encode workgroup normalises its element
+  // itself, instead of a k_histReduce / k_normalize launch.  Not for byte
+  // archives with a checksum (their partial checksums are summed by the
+  // normalisation kernels) nor for caller-supplied histograms.
+  const bool pro = runHist && !userHist && !rawCk && MB > 0 &&
+                   uint64_t(nb) * nW <= 2ull * residentSlots(reinterpret_cast<const void*>(&k_encode<FT, 0, true>),
+                                                             enc::kThreads, 0);
+  auto partHist = res.alloc<uint32_t>(s, runHist && !pro ? size_t(kSegs) * nb * chunks * kNumSymbols : 1);
   auto partCk = res.alloc<uint32_t>(s, rawCk ? size_t(nb) * chunks : 1);
   const uint32_t* chunkRows = preHist ? pre->rows : partHist.data();
   // first-level sums when elements have many chunks (k_histReduce)
   const uint32_t groups = divUp(chunks, kReduceRows);
-  const bool reduce2 = (runHist || preHist) && !preNorm && chunks > kReduceRows;
+  const bool reduce2 = (runHist || preHist) && !preNorm && !pro && chunks > kReduceRows;
   auto groupHist = res.alloc<uint32_t>(s, reduce2 ? size_t(kSegs) * nb * groups * kNumSymbols : 1);
   auto groupCk = res.alloc<uint32_t>(s, reduce2 && rawCk ? size_t(nb) * groups : 1);
   auto ck = res.alloc<uint32_t>(s, nb);
@@ -342,7 +353,6 @@ void encodeBatchDevice(StackDeviceMemory& res, int pb, bool useChecksum, uint32_
   const uint16_t* pdf = preNorm ? pre->pdf : pdfMem.data();
   auto slots = res.alloc<uint8_t>(s, size_t(kSegs) * nb * std::max(MB, 1u) * kSlotBytes);
   auto cw = res.alloc<uint32_t>(s, kFused ? 1 : size_t(kSegs) * nb * std::max(MB, 1u));
-  const uint32_t nW = std::max(1u, divUp(MB, EncCfg<FT>::kBlocksPerWG));
   // the normalisation runs in the last workgroup of the kernel that writes
   // an element's final partial rows (k_histReduce, or a k_hist of at most
   // 4096 workgroups), saving the k_normalize launch.  Each of those
@@ -350,12 +360,12 @@ void encodeBatchDevice(StackDeviceMemory& res, int pb, bool useChecksum, uint32_
   // round trip: with many (c3's k_hist: 65,536) that costs more than the
   // launch (c3 hist 0.74 -> 1.09 ms), so k_normalize runs there.
   const bool finalInReduce = reduce2;
-  const bool finalInHist = !reduce2 && runHist && uint64_t(chunks) * nb <= 4096;
+  const bool finalInHist = !reduce2 && !pro && runHist && uint64_t(chunks) * nb <= 4096;
   // k_encode's look-back flags (fused formats: one per element and encode
-  // workgroup, epoch-tagged, never zeroed) and the last-arrival counters, in
-  // this stream's sync arena
-  const size_t regions[kSyncRegions] = {0, kFused ? size_t(nb) * nW * 8 : 0, 0, 0, size_t(nb) * kSegs * 4};
-  SyncLease lease(res, s, regions);
+  // workgroup, epoch-tagged, never zeroed), the last-arrival counters and
+  // (pro) the histogram rows, in this stream's sync arena
+  const size_t regions[kSyncRegions] = {0, kFused ? size_t(nb) * nW * 8 : 0, 0, 0, size_t(nb) * kSegs * 4, 0};
+  SyncLease lease(res, s, regions, false, pro ? size_t(kSegs) * nb * kProRows * kNumSymbols * 4 : 0);
   NormArgs na;
   na.in = in;
   na.hist = userHist ? hist_dev : (reduce2 ? groupHist.data() : chunkRows);
@@ -379,7 +389,11 @@ void encodeBatchDevice(StackDeviceMemory& res, int pb, bool useChecksum, uint32_
       prof::Scope p("hist", s);
       dim3 g(chunks, ny);
       const NormArgs& nh = finalInHist ? naFinal : na;
-      if (rawCk) {
+      if (pro) {
+        k_hist<FT, false, true><<<g, kThreads, 0, s>>>(in, y0, nb, chunkWords, chunks,
+                                                       static_cast<uint32_t*>(lease.rows[0]), nullptr, na,
+                                                       static_cast<uint32_t*>(lease.rows[1]));
+      } else if (rawCk) {
         k_hist<FT, true><<<g, kThreads, 0, s>>>(in, y0, nb, chunkWords, chunks, partHist.data(),
                                                 partCk.data(), nh);
       } else {
@@ -404,7 +418,7 @@ void encodeBatchDevice(StackDeviceMemory& res, int pb, bool useChecksum, uint32_
                                           finalInReduce ? naFinal : na, kSegs);
       HIP_LAUNCH_CHECK();
     }
-    if (!finalInReduce && !finalInHist && !preNorm) {
+    if (!finalInReduce && !finalInHist && !preNorm && !pro) {
       prof::Scope p("normalize", s);
       dim3 g(ny, kSegs);
       k_normalize<<<g, kThreads, 0, s>>>(na, y0, nb);
@@ -418,8 +432,15 @@ void encodeBatchDevice(StackDeviceMemory& res, int pb, bool useChecksum, uint32_
                    spinCap(), deviceErrorWord(), sparseN};
       tail.epoch = lease.epoch;
       tail.skew = dispatchSkew();
-      k_encode<FT, 0><<<g, enc::kThreads, 0, s>>>(in, out, y0, nb, std::max(MB, 1u), table,
-                                               slots.data(), cw.data(), tail);
+      if (pro) {
+        tail.rows = static_cast<const uint32_t*>(lease.rows[0]);
+        tail.pdfOut = pdfMem.data();
+        k_encode<FT, 0, true><<<g, enc::kThreads, 0, s>>>(in, out, y0, nb, std::max(MB, 1u), table,
+                                                          slots.data(), cw.data(), tail);
+      } else {
+        k_encode<FT, 0><<<g, enc::kThreads, 0, s>>>(in, out, y0, nb, std::max(MB, 1u), table,
+                                                 slots.data(), cw.data(), tail);
+      }
       HIP_LAUNCH_CHECK();
     }
     if (!kFused) {

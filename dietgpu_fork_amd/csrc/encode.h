@@ -316,13 +316,21 @@ static __global__ __launch_bounds__(kThreads) void k_normalize(NormArgs a, uint3
 // lanes l and l + 16 of a wave half share a column.
 // ---------------------------------------------------------------------------
 constexpr int kHistCols = 32;
+// kRows (small three-kernel grids, k_encode's prologue normalisation):
+// chunk c adds its counts with atomics into row c % kProRows of
+// [segs][nb][kProRows][256] (this call's zeroed buffer of the sync arena),
+// so the encoder sums kProRows rows instead of a k_histReduce / k_normalize
+// launch summing thousands; zero bins add nothing.  `zeroNext`: the same
+// layout in the other buffer, zeroed here for the next call (SyncLease::rows).
+constexpr uint32_t kProRows = 64;
 
-template <int FT, bool kChecksum>
+template <int FT, bool kChecksum, bool kRows = false>
 __global__ __launch_bounds__(kThreads) void k_hist(BatchDesc in, uint32_t batchOffset,
                                                    uint32_t numInBatch, uint32_t chunkWords,
                                                    uint32_t chunksPerElem,
                                                    uint32_t* __restrict__ partHist,
-                                                   uint32_t* __restrict__ partCk, NormArgs na) {
+                                                   uint32_t* __restrict__ partCk, NormArgs na,
+                                                   uint32_t* __restrict__ zeroNext = nullptr) {
   using WordT = typename FloatTraits<FT>::WordT;
   constexpr int kSegs = FloatTraits<FT>::kSegs;
   // two segments (fp64): 16 columns each, so the counters take 32 KB and
@@ -414,9 +422,17 @@ __global__ __launch_bounds__(kThreads) void k_hist(BatchDesc in, uint32_t batchO
     uint32_t sum = 0;
 #pragma unroll
     for (int k = 0; k < kHistCols; ++k) sum += hs[s][tid * kHistCols + ((k + tid) & (kHistCols - 1))];
-    gp<uint32_t> dst = G(partHist) + ((uint64_t(s) * numInBatch + b) * chunksPerElem + c) * kNumSymbols + tid;
-    if (na.arrive) stSc1(dst, sum);  // read by this launch's last arrival
-    else *dst = sum;
+    if constexpr (kRows) {
+      const uint64_t row = (uint64_t(s) * numInBatch + b) * kProRows + (c & (kProRows - 1));
+      if (sum) __hip_atomic_fetch_add(G(partHist) + row * kNumSymbols + tid, sum, __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_AGENT);
+      for (uint32_t r = c; r < kProRows; r += chunksPerElem)
+        G(zeroNext)[((uint64_t(s) * numInBatch + b) * kProRows + r) * kNumSymbols + tid] = 0;
+    } else {
+      gp<uint32_t> dst = G(partHist) + ((uint64_t(s) * numInBatch + b) * chunksPerElem + c) * kNumSymbols + tid;
+      if (na.arrive) stSc1(dst, sum);  // read by this launch's last arrival
+      else *dst = sum;
+    }
   }
   if constexpr (kChecksum) {
     ck = (ck ^ (ck >> 8) ^ (ck >> 16) ^ (ck >> 24)) & 0xffu;
@@ -776,7 +792,64 @@ struct EncTail {
   const uint32_t* sparseN = nullptr;
   uint32_t skew = 0;  // test hook: emulated out-of-order start (skewDelay, device.h)
   uint32_t epoch = 0;  // this call's epoch: the flags are epoch-tagged (sync arena), never zeroed
+  // prologue normalisation (k_encode<.., kPro>): k_hist's kProRows rows per
+  // (segment, element), and (fp64) where workgroup 0 leaves the pdf rows for
+  // k_coalesce
+  const uint32_t* rows = nullptr;
+  uint16_t* pdfOut = nullptr;
 };
+
+// Prologue normalisation of k_encode (small grids): every workgroup sums its
+// element's kProRows histogram rows per segment (k_hist<.., kRows>) and
+// normalises them itself -- wave s segment s, in registers (normalizeWave)
+// -- into its LDS encode table and pdf row.  The redundant work is a few
+// microseconds at the start of a one-generation grid; the k_histReduce /
+// k_normalize launch it replaces (a chain of dependent round trips over
+// thousands of rows, plus its launch) cost ~10 us per call (c4 fp64,
+// batch-1 float tensors).  red4: S * 256 16 B scratch.  Whole workgroup;
+// the caller synchronises before reading tblS / pdfS.
+template <int S>
+__device__ __forceinline__ void proNormalize(gp<const uint32_t> rows, uint32_t nb, uint32_t b, uint32_t n,
+                                             int pb, lp<u32x4> red4, uint32_t (*tblS)[kNumSymbols * 4],
+                                             uint16_t (*pdfS)[kNumSymbols]) {
+  const uint32_t t = threadIdx.x, q = t & 63, st = t >> 6;
+  constexpr uint32_t kPer = kProRows / 4;  // rows per thread (rows congruent to st mod 4)
+  constexpr uint32_t kB = 8;               // loads in flight per segment
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    gp<const u32x4> p = (gp<const u32x4>)(rows + (uint64_t(s) * nb + b) * kProRows * kNumSymbols) + q;
+    u32x4 acc = u32x4{0, 0, 0, 0};
+#pragma unroll
+    for (uint32_t k0 = 0; k0 < kPer; k0 += kB) {
+      u32x4 v[kB];
+#pragma unroll
+      for (uint32_t k = 0; k < kB; ++k) v[k] = p[uint64_t(st + 4 * (k0 + k)) * (kNumSymbols / 4)];
+#pragma unroll
+      for (uint32_t k = 0; k < kB; ++k) acc += v[k];
+    }
+    red4[s * kThreads + st * 64 + q] = acc;
+  }
+  __syncthreads();
+  const uint32_t w = t >> 6;
+  if (w < uint32_t(S)) {
+    u32x4 a = red4[w * kThreads + q];
+#pragma unroll
+    for (uint32_t k = 1; k < 4; ++k) a += red4[w * kThreads + k * 64 + q];
+    uint32_t c[4] = {a.x, a.y, a.z, a.w}, cdf[4] = {0, 0, 0, 0};
+    if (n != 0) {
+      normalizeWave(c, cdf, n, pb);
+    } else {  // (ans/GpuANSStatistics.cuh:193-195: an empty element's table is zero)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) c[j] = 0;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint4 e = n != 0 ? encTableEntryReg(c[j], cdf[j], pb) : make_uint4(0, 0, 0, 0);
+      *(lp<u32x4>)&tblS[w][4 * (4 * q + j)] = u32x4{e.x, e.y, e.z, e.w};
+    }
+    *(lp<u32x2>)&pdfS[w][4 * q] = u32x2{c[0] | (c[1] << 16), c[2] | (c[3] << 16)};
+  }
+}
 
 // bytes of a sparse archive before its dense part: 16 B header, bitmap
 // padded to 16 (float/GpuSparseFloatCompress.cuh)
@@ -844,7 +917,7 @@ __device__ __forceinline__ uint32_t lookBackPoison(gp<uint64_t> f, uint32_t x, u
 // raw section's rounding tails.  Whole workgroup.
 template <int FT>
 __device__ __forceinline__ void writeHeadFixed(gp<uint8_t> base, gp<uint8_t> o, uint32_t n, uint32_t nBlocks,
-                               const EncTail& t, uint32_t b) {
+                               const EncTail& t, uint32_t b, uint16_t pdfOfTid) {
   const uint32_t tid = threadIdx.x;
   const bool ansCk = FT == 0 && t.useChecksum;
   if (tid == 0) {
@@ -867,7 +940,7 @@ __device__ __forceinline__ void writeHeadFixed(gp<uint8_t> base, gp<uint8_t> o, 
       fh[7] = 0;
     }
   }
-  ((gp<uint16_t>)(o + kANSHeaderBytes))[tid] = G(t.pdf)[uint64_t(b) * kNumSymbols + tid];
+  ((gp<uint16_t>)(o + kANSHeaderBytes))[tid] = pdfOfTid;
   if constexpr (FT != 0) {
     if (tid < 16) {
       gp<uint8_t> raw = base + 32;
@@ -902,7 +975,7 @@ __device__ __forceinline__ void writeHeadTotal(gp<uint8_t> base, gp<uint8_t> o, 
 // (kFused): writes the whole archive (states straight to it, words via the
 // slots, see EncTail).  fp64: writes per block slot states, slot words and
 // cw[] (word count) for k_coalesce.
-template <int FT, int KK>
+template <int FT, int KK, bool kPro = false>
 __global__ __launch_bounds__(enc::kThreads) void k_encode(BatchDesc in, BatchDesc out,
                                                           uint32_t batchOffset,
                                                           uint32_t numInBatch, uint32_t MB,
@@ -921,6 +994,8 @@ __global__ __launch_bounds__(enc::kThreads) void k_encode(BatchDesc in, BatchDes
   __shared__ uint32_t cwE[Cfg::kBlocksPerWG];
   __shared__ uint32_t flE[Cfg::kBlocksPerWG];
   __shared__ uint32_t preE[Cfg::kBlocksPerWG];
+  __shared__ __attribute__((aligned(16))) uint16_t pdfS[kPro ? S : 1][kNumSymbols];
+  static_assert(sizeof(ringS) >= S * kThreads * 16, "prologue scratch in the rings");
 
   const uint32_t tid = threadIdx.x;
   // (chunk, element) = blockIdx: the fused look-back waits on lower chunks of
@@ -934,18 +1009,28 @@ __global__ __launch_bounds__(enc::kThreads) void k_encode(BatchDesc in, BatchDes
   const uint32_t n = in.size(b);
   const uint32_t nBlocks = divUp(n, kBlockSize);
   const uint32_t first = wx * Cfg::kBlocksPerWG;
-  // workgroup 0 of an element always runs (headers, empty elements)
-  if (first >= nBlocks && (!kFused || wx != 0)) return;
+  // workgroup 0 of an element always runs (headers, empty elements; with
+  // kPro also the pdf rows k_coalesce reads)
+  if (first >= nBlocks && ((!kFused && !kPro) || wx != 0)) return;
   gp<uint8_t> base = startOf(out, b);
   gp<uint8_t> o = base + (FT == 0 ? 0u : 32u + floatRawBytes(FT, n));  // ANS archive
   gp<uint8_t> states = o + kANSHeaderBytes + kPdfBytes;
   gp<uint2> bwords = (gp<uint2>)(states + uint64_t(kStateBytesPerBlock) * nBlocks);
+  if constexpr (kPro) {
+    proNormalize<S>(G(tail.rows), numInBatch, b, n, tail.pb, (lp<u32x4>)&ringS[0][0], tblS, pdfS);
+    __syncthreads();
+    if (!kFused && wx == 0) {
 #pragma unroll
-  for (int s = 0; s < S; ++s) {
-    const uint4 t = ld16(G(table) + (uint64_t(s) * numInBatch + b) * kNumSymbols + tid);
-    *(lp<u32x4>)&tblS[s][4 * tid] = u32x4{t.x, t.y, t.z, t.w};
+      for (int s = 0; s < S; ++s) G(tail.pdfOut)[(uint64_t(s) * numInBatch + b) * kNumSymbols + tid] = pdfS[s][tid];
+    }
+  } else {
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      const uint4 t = ld16(G(table) + (uint64_t(s) * numInBatch + b) * kNumSymbols + tid);
+      *(lp<u32x4>)&tblS[s][4 * tid] = u32x4{t.x, t.y, t.z, t.w};
+    }
+    __syncthreads();
   }
-  __syncthreads();
 
   const uint32_t w = readfirst(tid >> 6), lane = tid & 63, h = lane >> 5, l = lane & 31;
   const uint32_t blk0 = first + w * Cfg::kBlocksPerWave;
@@ -1157,7 +1242,9 @@ __global__ __launch_bounds__(enc::kThreads) void k_encode(BatchDesc in, BatchDes
         }
       }
     }
-    if (wx == 0) writeHeadFixed<FT>(base, o, n, nBlocks, tail, b);
+    if (wx == 0)
+      writeHeadFixed<FT>(base, o, n, nBlocks, tail, b,
+                         kPro ? pdfS[0][tid] : G(tail.pdf)[uint64_t(b) * kNumSymbols + tid]);
     __syncthreads();
     if (tid < nk) {
       const uint32_t k = first + tid;

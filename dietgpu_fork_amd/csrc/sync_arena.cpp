@@ -27,6 +27,9 @@ struct Arena {
   // path) still takes an epoch, so the counter a later k_pcompress call uses
   // can be the dirty one: it is then zeroed here, stream-ordered.
   uint32_t ctrDirty = 0;
+  // kSyncRows: bytes at the start of row buffer k (the region's halves)
+  // known to be zero
+  size_t rowsClean[2] = {0, 0};
 };
 
 using Key = std::tuple<int, hipStream_t, size_t>;
@@ -49,10 +52,12 @@ void setDispatchSkew(uint32_t ticks) { gDispatchSkew.store(ticks); }
 uint32_t dispatchSkew() { return gDispatchSkew.load(); }
 
 SyncLease::SyncLease(StackDeviceMemory& res, hipStream_t stream, const size_t (&bytesIn)[kSyncRegions],
-                     bool dequeue) {
+                     bool dequeue, size_t rowsBytes) {
   size_t bytes[kSyncRegions];
   for (int k = 0; k < kSyncRegions; ++k) bytes[k] = bytesIn[k];
   bytes[kSyncCounters] = std::max(bytes[kSyncCounters], kSyncCounterBytes);
+  rowsBytes = roundUp64(rowsBytes, 256);
+  bytes[kSyncRows] = 2 * rowsBytes;
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
   HIP_CHECK(hipStreamIsCapturing(stream, &cs));
   if (cs != hipStreamCaptureStatusNone) {
@@ -69,6 +74,8 @@ SyncLease::SyncLease(StackDeviceMemory& res, hipStream_t stream, const size_t (&
       off += roundUp64(std::max<size_t>(bytes[k], 8), 256);
     }
     epoch = 1;
+    rows[0] = base[kSyncRows];
+    rows[1] = static_cast<uint8_t*>(base[kSyncRows]) + rowsBytes;
     return;
   }
   int dev = 0;
@@ -96,6 +103,7 @@ SyncLease::SyncLease(StackDeviceMemory& res, hipStream_t stream, const size_t (&
       zeroAsync(a->ptr[k], want, stream);
       a->bytes[k] = want;
       if (k == kSyncCounters) a->ctrDirty = 0;
+      if (k == kSyncRows) a->rowsClean[0] = a->rowsClean[1] = want / 2;
     }
   }
   a->epoch = (a->epoch + 1) & kEpochMask;
@@ -103,6 +111,7 @@ SyncLease::SyncLease(StackDeviceMemory& res, hipStream_t stream, const size_t (&
     for (int k = 0; k < kSyncRegions; ++k) zeroAsync(a->ptr[k], a->bytes[k], stream);
     a->epoch = 1;
     a->ctrDirty = 0;
+    a->rowsClean[0] = a->rowsClean[1] = a->bytes[kSyncRows] / 2;
   }
   if (dequeue) {  // a k_pcompress call: its counter must start at zero
     const uint32_t mine = a->epoch & 1u;
@@ -112,6 +121,15 @@ SyncLease::SyncLease(StackDeviceMemory& res, hipStream_t stream, const size_t (&
   }
   for (int k = 0; k < kSyncRegions; ++k) base[k] = a->ptr[k];
   epoch = a->epoch;
+  if (rowsBytes) {  // buffer epoch & 1 now, the other one for the next call
+    const uint32_t mine = a->epoch & 1u;
+    const size_t half = a->bytes[kSyncRows] / 2;
+    rows[0] = static_cast<uint8_t*>(a->ptr[kSyncRows]) + mine * half;
+    rows[1] = static_cast<uint8_t*>(a->ptr[kSyncRows]) + (mine ^ 1u) * half;
+    if (a->rowsClean[mine] < rowsBytes) zeroAsync(rows[0], rowsBytes, stream);
+    a->rowsClean[mine] = 0;            // accumulated into by this call
+    a->rowsClean[mine ^ 1u] = rowsBytes;  // zeroed by this call's k_hist
+  }
 }
 
 }  // namespace dietgpu

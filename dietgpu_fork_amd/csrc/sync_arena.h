@@ -38,8 +38,13 @@ constexpr uint32_t kEpochMask = 0xffffu;
 // a partial's epoch -- cannot happen whatever the shapes of earlier calls).
 // kSyncArrive holds the three-kernel path's last-arrival counters (NormArgs,
 // encode.h): untagged, they wrap back to zero at every element's last
-// arrival, so they are zero between calls.
-enum SyncRegion : int { kSyncCounters = 0, kSyncFlags, kSyncPartials, kSyncLog, kSyncArrive, kSyncRegions };
+// arrival, so they are zero between calls.  kSyncRows holds two buffers of
+// histogram rows that k_hist accumulates with atomics for the encoder's
+// prologue normalisation (small three-kernel grids): a call uses buffer
+// epoch & 1, which must start zeroed, and its k_hist zeroes the other one
+// for the next call (SyncLease::rows).
+enum SyncRegion : int { kSyncCounters = 0, kSyncFlags, kSyncPartials, kSyncLog, kSyncArrive, kSyncRows,
+                        kSyncRegions };
 // kSyncCounters layout: k_pcompress's two u64 dequeue counters.
 constexpr size_t kSyncCounterBytes = 16;
 
@@ -49,12 +54,17 @@ class SyncLease {
   // and `stream`, and this call's epoch (1 .. kEpochMask).
   // dequeue: the call runs k_pcompress, whose dequeue counter (epoch & 1)
   // must start at zero (see Arena::ctrDirty).
-  SyncLease(StackDeviceMemory& res, hipStream_t stream, const size_t (&bytes)[kSyncRegions], bool dequeue = false);
+  // rowsBytes > 0: the call accumulates rowsBytes of histogram rows in
+  // rows[0] (zero on entry) and zeroes the first rowsBytes of rows[1] for
+  // the next call (bytes[kSyncRows] is ignored).
+  SyncLease(StackDeviceMemory& res, hipStream_t stream, const size_t (&bytes)[kSyncRegions], bool dequeue = false,
+            size_t rowsBytes = 0);
 
   SyncLease(const SyncLease&) = delete;
   SyncLease& operator=(const SyncLease&) = delete;
 
   void* base[kSyncRegions] = {};
+  void* rows[2] = {};  // this call's row buffer, the next call's (rowsBytes > 0)
   uint32_t epoch = 0;
   bool capturing = false;
 
