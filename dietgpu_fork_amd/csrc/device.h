@@ -220,6 +220,24 @@ __device__ __forceinline__ u32x4 ldSc1x4(gp<const u32x4> p) {
   const uint64_t b = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   return u32x4{uint32_t(a), uint32_t(a >> 32), uint32_t(b), uint32_t(b >> 32)};
 }
+// Sixteen bytes of a tagged-granule row in ONE sc1 load (a buffer load: the
+// atomic-load path only has 8 B forms).  Every word carries its own epoch tag,
+// so the load need not be single-copy atomic.  base: wave-uniform; byteOff:
+// per lane, below 2^31.
+#if defined(__HIP_DEVICE_COMPILE__)
+using BufRsrc = __amdgpu_buffer_rsrc_t;
+__device__ __forceinline__ BufRsrc bufOf(gp<const void> base) {
+  // dword 3: the raw-buffer format word of gfx9 (CK_BUFFER_RESOURCE_3RD_DWORD)
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(const void*)base, 0, 0x7fffffff, 0x00020000);
+}
+__device__ __forceinline__ u32x4 ldSc1x4(BufRsrc r, uint32_t byteOff) {
+  return __builtin_amdgcn_raw_buffer_load_b128(r, byteOff, 0, /*sc1*/ 16);
+}
+#else  // host pass of the kernel templates: never called
+struct BufRsrc {};
+__device__ __forceinline__ BufRsrc bufOf(gp<const void>) { return {}; }
+__device__ __forceinline__ u32x4 ldSc1x4(BufRsrc, uint32_t) { return u32x4{0, 0, 0, 0}; }
+#endif
 __device__ __forceinline__ void stSc1(gp<uint32_t> p, uint32_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }

@@ -694,6 +694,8 @@ __global__ __launch_bounds__(pc::kThreads) __attribute__((amdgpu_waves_per_eu(4,
     }
     // payload: 16 B vectors over the item's contiguous archive range; the
     // source is the block's ring, or its slot for words spilled before the end
+    // (per-wave block lists with wave-uniform block parameters measured +1
+    // us)
     gp<uint4> dst = (gp<uint4>)((gp<uint8_t>)(bwords + roundUp(it.nBlocks, 2)) + 2ull * preE[0]);
     const uint32_t nv = (preE[nk - 1] + roundUp(cwE[nk - 1], 8) - preE[0]) / 8;
     for (uint32_t v = t; v < nv; v += kPT) {
@@ -836,11 +838,11 @@ __global__ __launch_bounds__(pc::kThreads) __attribute__((amdgpu_waves_per_eu(4,
     if (hasL) {
       const uint32_t lane = laneNow();
       const PItem L = itemOf(iL, A(), IN());
-      gp<const u32x4> hp = (gp<const u32x4>)(G(A().part) + uint64_t(L.tb) * kNumSymbols) + lane;
+      const BufRsrc hb = bufOf(G(A().part) + uint64_t(L.tb) * kNumSymbols);
 #pragma unroll
       for (uint32_t m = 0; m < kFirst; ++m) {
         const uint32_t k = w + pc::kWaves * m;
-        pa[m] = k < L.team ? ldSc1x4(hp + uint64_t(k) * (kNumSymbols / 4)) : u32x4{0, 0, 0, 0};
+        pa[m] = k < L.team ? ldSc1x4(hb, (k * 64 + lane) * 16) : u32x4{0, 0, 0, 0};
       }
       if constexpr (kCk) {
         if (w == 0) ckv = lane < L.team ? ldSc1(G(A().partCk) + L.tb + lane) : 0u;
@@ -873,7 +875,7 @@ __global__ __launch_bounds__(pc::kThreads) __attribute__((amdgpu_waves_per_eu(4,
       const uint32_t lane = laneNow();
       const PItem L = itemOf(iL, A(), IN());
       const uint32_t ep = A().epoch;
-      gp<const u32x4> hp = (gp<const u32x4>)(G(A().part) + uint64_t(L.tb) * kNumSymbols) + lane;
+      const BufRsrc hb = bufOf(G(A().part) + uint64_t(L.tb) * kNumSymbols);
       auto tagged = [&](const u32x4& v) __attribute__((always_inline)) -> bool {
         return (v.x >> 16) == ep && (v.y >> 16) == ep && (v.z >> 16) == ep && (v.w >> 16) == ep;
       };
@@ -912,7 +914,7 @@ __global__ __launch_bounds__(pc::kThreads) __attribute__((amdgpu_waves_per_eu(4,
 #pragma unroll
         for (uint32_t m = 0; m < kPer; ++m) {
           if ((miss >> m) & 1u) {
-            const u32x4 v = ldSc1x4(hp + uint64_t(w + pc::kWaves * m) * (kNumSymbols / 4));
+            const u32x4 v = ldSc1x4(hb, ((w + pc::kWaves * m) * 64 + lane) * 16);
             if (tagged(v)) {
               take(v);
               miss &= ~(1u << m);

@@ -190,7 +190,59 @@ PLAINALL = PLAINPART + [
 # DESIGN.md section 7).
 PSKEW = [(P, "  __syncthreads();  // histogram zeroed\n",
           "  if (tid == 0) skewDelay(100);\n  __syncthreads();  // histogram zeroed\n")]
+# round 5: the decoder's raw float bytes loaded TWO 8-step segments ahead
+# (three register buffers), for archives read cold from HBM
+DEC2A = [(DH, """      int32_t g = min(nSeg, int32_t(nFull)) - 1;  // rvA holds segment g's bytes
+      for (; g >= 1; g -= 2) {
+        fullSeg(g, rvA, rvB);
+        fullSeg(g - 1, rvB, rvA);
+      }
+      if (g == 0) fullSeg(0, rvA, rvB);""", """      uint32_t rvC[K][R];
+      auto fullSeg2 = [&](int32_t g, const uint32_t (&cur)[K][R], uint32_t (&nxt2)[K][R]) {
+        if constexpr (BAL)
+          setPrioRemaining((chunksPerWG - 1 - pass) * uint32_t(nSeg) + uint32_t(g), chunksPerWG * uint32_t(nSeg));
+        if (g > 1) loadRaw(g - 2, true, nxt2);
+#pragma unroll
+        for (int grp = int(dec::kSegSteps / dec::kUnroll) - 1; grp >= 0; --grp) {
+#pragma unroll
+          for (int c = 0; c < K; ++c)
+#pragma unroll
+            for (int s = 0; s < S; ++s) ringEnsure(st[c][s], lane, kVec);
+#pragma unroll
+          for (int u = int(dec::kUnroll) - 1; u >= 0; --u) {
+            const int tr = grp * int(dec::kUnroll) + u;
+            uint32_t e0[K * S];
+            decStepAll<false, K * S>(chains, allValid, lutC, mask, pb, hv, e0);
+#pragma unroll
+            for (int c = 0; c < K; ++c)
+#pragma unroll
+              for (int s = 0; s < S; ++s) segLane[c][s][tr * 32] = uint16_t(e0[c * S + s] >> 16);
+          }
+        }
+        __builtin_amdgcn_wave_barrier();
+        join(g, true, cur);
+        __builtin_amdgcn_wave_barrier();
+      };
+      (void)fullSeg;
+      int32_t g = min(nSeg, int32_t(nFull)) - 1;  // rvA holds segment g's bytes
+      if (g >= 1) loadRaw(g - 1, true, rvB);
+      for (; g >= 2; g -= 3) {
+        fullSeg2(g, rvA, rvC);
+        fullSeg2(g - 1, rvB, rvA);
+        fullSeg2(g - 2, rvC, rvB);
+      }
+      if (g == 1) {
+        fullSeg2(1, rvA, rvC);
+        fullSeg2(0, rvB, rvC);
+      } else if (g == 0) {
+        fullSeg2(0, rvA, rvC);
+      }""")]
 VARS = {
+    "dec2a": DEC2A,
+    # the same with the SGPR count held at 80 (84 SGPRs admit 7 workgroups
+    # per CU instead of 8, MI355X_MICROARCH.md "Residency")
+    "dec2a80": DEC2A + [(DH, "__global__ __launch_bounds__(dec::kThreads) void k_decode(",
+                         "__global__ __launch_bounds__(dec::kThreads) __attribute__((amdgpu_num_sgpr(80))) void k_decode(")],
     "pskew": PSKEW,
     # VERDICT r4 item 4: a single-read c3 (4 MiB byte elements, teams of
     # 128 items) through k_pcompress, measured instead of extrapolated
