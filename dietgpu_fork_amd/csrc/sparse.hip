@@ -191,8 +191,10 @@ __device__ __forceinline__ void sparseCountTile(const BatchDesc& in, gp<uint8_t>
 // list.  (Normalising in the element's last-arriving tile instead of the
 // dense codec's k_normalize launch made every tile pay a store drain and a
 // counter round trip: c4 1 x 15M fp32 compress 70 -> 95 us.)
+// (at most 80 SGPRs: 86-94 admit 7 workgroups per CU instead of 8,
+// MI355X_MICROARCH.md, Residency)
 template <int FT, bool kVec, bool kHist>
-__global__ __launch_bounds__(kThreads) void k_sparseCount(BatchDesc in, BatchDesc outD,
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_num_sgpr(80))) void k_sparseCount(BatchDesc in, BatchDesc outD,
                                                           uint32_t batchOffset, uint32_t numInBatch,
                                                           uint32_t tilesPerElem,
                                                           uint32_t* __restrict__ tileCounts,
