@@ -111,3 +111,31 @@ def test_epoch_wraparound(env):
     s.synchronize()
     assert C.device_error_count(reset=True) == 0
     assert C.barrier_fallback_count(reset=True) == 0
+
+
+def test_prenormalised_sparse_after_single_pass(env):
+    """The sparse compressor's dense list goes through the three-kernel
+    encoder with a caller-normalised table (preNorm: no k_normalize, the
+    encoder's fused look-back flags in the same kSyncFlags region): run it
+    straight after single-pass calls (sentinel-filled outputs) on the same
+    stream, alternating, and compare both with the oracle's archives."""
+    N, C = env
+    ws = C.Workspace(256 << 20)
+    s = torch.cuda.Stream()
+    a = Batch(N, [300000, 524288, 70001], seed=31, aligned=True)
+    from tests.util import sparsify
+
+    n = 3_000_000  # 30 % nonzeros: a list of > 2^20 words (three-kernel, preNorm)
+    w = sparsify(float_words(3, n, seed=33), frac_zero=0.7, seed=34)
+    ref = O.sparse_compress(w, 3)
+    x = torch.from_numpy(w.view(np.int32)).to(DEV).view(torch.float32)
+    C.device_error_count(reset=True)
+    with torch.cuda.stream(s):
+        for k in range(4):
+            a.compress(ws, s)
+            out, sizes = C.sparse_compress([x], ws=ws)
+            s.synchronize()
+            a.check()
+            assert int(sizes[0]) == ref.size
+            np.testing.assert_array_equal(out[0, : ref.size].cpu().numpy(), ref, err_msg=f"round {k}")
+    assert C.device_error_count(reset=True) == 0
