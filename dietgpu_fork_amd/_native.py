@@ -41,6 +41,7 @@ def _declare(L):
         "dietgpu_set_spin_cap": (None, [c_u32]),
         "dietgpu_set_barrier_budget": (None, [c_u32]),
         "dietgpu_set_dispatch_skew": (None, [c_u32]),
+        "dietgpu_set_compress_path": (None, [c_int]),
         "dietgpu_test_occupy": (c_int, [P, c_u32, c_u32, c_u32]),
         "dietgpu_test_histogram": (c_int, [vp, c_u32, P, c_u32, c_u32, P, P]),
         "dietgpu_version": (ctypes.c_char_p, []),
@@ -87,7 +88,7 @@ def _declare(L):
     }
     # test hooks absent from older builds (same-box A/B of earlier libraries)
     optional = {"dietgpu_set_barrier_budget", "dietgpu_set_dispatch_skew", "dietgpu_test_occupy", "dietgpu_test_histogram",
-                "dietgpu_barrier_fallback_count"}
+                "dietgpu_barrier_fallback_count", "dietgpu_set_compress_path"}
     for name, (res, args) in sig.items():
         if name in optional and not hasattr(L, name):
             continue

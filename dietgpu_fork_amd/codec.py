@@ -3,6 +3,8 @@ points), used by tests and bench.py.  Every function runs the HIP kernels on
 the torch current stream and returns device tensors; nothing here computes on
 the CPU.
 """
+import contextlib
+
 import torch
 
 from . import _native as N
@@ -87,6 +89,26 @@ def set_barrier_budget(ticks):
     its team before counting the element itself (default 20000; 0 forces the
     fallback on every team wait)."""
     N.lib().dietgpu_set_barrier_budget(int(ticks))
+
+
+_PATHS = {"auto": 0, "single-pass": 1, "three-kernel": 2}
+
+
+def set_compress_path(mode):
+    """Test hook: "auto" (default: the size rule), "single-pass" (k_pcompress
+    whenever the batch is eligible) or "three-kernel" (always k_hist ->
+    k_encode).  Archives are identical whatever the mode."""
+    N.lib().dietgpu_set_compress_path(_PATHS[mode])
+
+
+@contextlib.contextmanager
+def compress_path(mode):
+    """set_compress_path(mode) for the body, "auto" after it."""
+    set_compress_path(mode)
+    try:
+        yield
+    finally:
+        set_compress_path("auto")
 
 
 # ------------------------------------------------------------------ ANS ----

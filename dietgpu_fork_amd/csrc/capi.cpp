@@ -320,6 +320,7 @@ uint32_t dietgpu_barrier_fallback_count(int reset) {
 void dietgpu_set_spin_cap(uint32_t polls) { setSpinCap(polls); }
 void dietgpu_set_barrier_budget(uint32_t ticks) { setBarrierBudget(ticks); }
 void dietgpu_set_dispatch_skew(uint32_t ticks) { setDispatchSkew(ticks); }
+void dietgpu_set_compress_path(int mode) { setCompressPath(mode < 0 || mode > 2 ? 0 : mode); }
 
 int dietgpu_test_occupy(void* stream, uint32_t micros, uint32_t workgroups, uint32_t lds_bytes) {
   return guarded([&] {

@@ -200,9 +200,59 @@ uint32_t barrierFallbackCount(bool reset) { return readErrorWord(1, reset); }
 // formats without a caller-supplied histogram, elements of at most
 // pc::kMaxTeam items (1 MiB of symbols).  One generation of resident
 // workgroups pulls items off the work queue.
-bool persistentFits(uint32_t maxWords) {
-  return divUp(divUp(maxWords, kBlockSize), pc::kBlocksPerItem) <= pc::kMaxTeam;
+// Teams of k_pcompress for nb elements of maxWords: team size, teams per
+// round (XCD-aligned when that fits, see compressPersistent) and whether
+// they are XCD-aligned.  team == 0: the elements are too large.
+struct PersistentPlan {
+  uint32_t team = 0, teamsPerRound = 0, rounds = 0;
+  bool xcd = false;
+};
+
+template <int FT>
+PersistentPlan planPersistent(uint32_t nb, uint32_t maxWords) {
+  PersistentPlan p;
+  const uint32_t team = std::max(1u, divUp(divUp(maxWords, kBlockSize), pc::kBlocksPerItem));
+  if (team > pc::kMaxTeam || nb == 0) return p;
+  // (the instances have the same resources: one occupancy query)
+  const uint32_t slots = residentSlots(reinterpret_cast<const void*>(&k_pcompress<FT, false, true>), pc::kThreads, 0);
+  // rounds of whole teams, balanced: R rounds of ceil(nb / R) teams
+  const uint32_t maxTeams = std::max(1u, slots / team);
+  p.team = team;
+  p.rounds = divUp(nb, maxTeams);
+  p.teamsPerRound = divUp(nb, p.rounds);
+  // XCD-aligned teams (kXcd, pcompress.h) whenever the teams per round round
+  // up to a multiple of 8 within the resident grid (never more rounds; a
+  // batch of fewer than 8 elements gets idle teams that exit at once), so
+  // the partial histograms stay in one L2.  Otherwise (e.g. 33 elements of
+  // 31 items in 1,024 slots) the team members span XCDs and the partials go
+  // out write-through.
+  p.xcd = roundUp(p.teamsPerRound, 8) <= maxTeams;
+  if (p.xcd) p.teamsPerRound = roundUp(p.teamsPerRound, 8);
+  return p;
 }
+
+// Whether the single-pass compressor beats the three-kernel path (k_hist ->
+// k_encode with prologue normalisation) for a batch.  At most 256 items, or
+// one round whose teams cannot be XCD-aligned, leave most of the chip idle
+// while a team's members wait on each other's partial histograms; there the
+// chip-wide histogram pass plus the encoder are faster (round 5, bf16:
+// 1 x 1e6 words 30.7 -> 22.9 us, 8 x 524288 26.9 -> 25.1 us, 33 x 1e6
+// 48.9 -> 46.9 us; 16 x 1e6, 496 items, stays single-pass: 33.5 against
+// 37.1 us).
+// (dietgpu_set_compress_path overrides the rule: test hook.)
+template <int FT>
+bool persistentPreferred(uint32_t nb, uint32_t maxWords) {
+  const int mode = compressPath();
+  if (mode == 2) return false;
+  const PersistentPlan p = planPersistent<FT>(nb, maxWords);
+  if (p.team == 0) return false;
+  if (mode == 1) return true;
+  if (uint64_t(p.team) * nb <= 256) return false;
+  return !(p.rounds == 1 && !p.xcd);
+}
+template bool persistentPreferred<1>(uint32_t, uint32_t);
+template bool persistentPreferred<2>(uint32_t, uint32_t);
+template bool persistentPreferred<3>(uint32_t, uint32_t);
 
 template <int FT, bool kCk, bool kXcd>
 void launchPersistent(uint32_t grid, hipStream_t s, const DeviceTables* tabs, const BatchDesc& in,
@@ -216,27 +266,14 @@ bool compressPersistent(StackDeviceMemory& res, int pb, bool useChecksum, uint32
                         const BatchDesc& in, uint32_t maxSize, const BatchDesc& out,
                         uint32_t* outSize_dev, hipStream_t s, const DeviceTables* tabs,
                         const uint32_t* sparseN) {
-  const uint32_t MB = divUp(maxSize, kBlockSize);
-  const uint32_t team = std::max(1u, divUp(MB, pc::kBlocksPerItem));
-  if (team > pc::kMaxTeam) return false;
+  const PersistentPlan plan = planPersistent<FT>(nb, maxSize);
+  const uint32_t team = plan.team;
+  if (team == 0) return false;
   const uint64_t items64 = uint64_t(team) * nb;
   DG_CHECK(items64 < (1ull << 30), "batch too large for one compress call");
   const uint32_t items = uint32_t(items64);
-  // (both instances have the same resources: one occupancy query)
-  const uint32_t slots = residentSlots(reinterpret_cast<const void*>(&k_pcompress<FT, kCk, true>), pc::kThreads, 0);
-  // rounds of whole teams, balanced: R rounds of ceil(nb / R) teams
-  const uint32_t maxTeams = std::max(1u, slots / team);
-  const uint32_t rounds = divUp(nb, maxTeams);
-  uint32_t teamsPerRound = divUp(nb, rounds);
-  // XCD-aligned teams (kXcd, pcompress.h) whenever the teams per round round
-  // up to a multiple of 8 within the resident grid (never more rounds; a
-  // batch of fewer than 8 elements gets idle teams that exit at once), so
-  // the partial histograms stay in one L2.  Otherwise (e.g. 33 elements of
-  // 31 items in 1,024 slots) the team members span XCDs and the partials go
-  // out write-through.
-  const bool xcdTeams = roundUp(teamsPerRound, 8) <= maxTeams;
-  if (xcdTeams) teamsPerRound = roundUp(teamsPerRound, 8);
-  const uint32_t grid = teamsPerRound * team;
+  const bool xcdTeams = plan.xcd;
+  const uint32_t grid = plan.teamsPerRound * team;
 
   auto slotMem = res.alloc<uint8_t>(s, size_t(grid) * pc::kBlocksPerItem * kSlotDataBytes);
   auto ck = res.alloc<uint32_t>(s, FT != 0 && useChecksum ? nb : 1);
@@ -316,7 +353,9 @@ void encodeBatchDevice(StackDeviceMemory& res, int pb, bool useChecksum, uint32_
   const bool rawCk = FT == 0 && useChecksum;
   const uint32_t nW = std::max(1u, divUp(MB, EncCfg<FT>::kBlocksPerWG));
   if constexpr (kFused) {
-    if (!userHist && inAligned16) {
+    // (byte archives with a checksum stay single-pass: the three-kernel path
+    // has no prologue normalisation for them)
+    if (!userHist && inAligned16 && ((rawCk && compressPath() != 2) || persistentPreferred<FT>(nb, maxSize))) {
       const bool done = rawCk ? compressPersistent<FT, FT == 0>(res, pb, useChecksum, nb, inArg,
                                                                  maxSize, outArg, outSize_dev, s, tabs, sparseN)
                               : compressPersistent<FT, false>(res, pb, useChecksum, nb, inArg, maxSize,

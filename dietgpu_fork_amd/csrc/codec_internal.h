@@ -32,9 +32,11 @@ void floatCompressDescs(StackDeviceMemory& res, const FloatCompressConfig& confi
                         bool inAligned16 = false, const PartialHist* pre = nullptr,
                         const uint32_t* sparseN = nullptr);
 
-// The single-pass compressor (k_pcompress) takes float elements of at most
-// this many words (and 16 B-aligned inputs).
-bool persistentFits(uint32_t maxWords);
+// Whether encodeBatchDevice compresses nb 16 B-aligned elements of at most
+// maxWords words of a single-segment format (FT 0-3) with the single-pass
+// compressor (k_pcompress) rather than the three-kernel path.
+template <int FT>
+bool persistentPreferred(uint32_t nb, uint32_t maxWords);
 
 FloatDecompressStatus floatDecompressDescs(StackDeviceMemory& res,
                                            const FloatDecompressConfig& config, uint32_t nb,

@@ -538,29 +538,38 @@ __global__ __launch_bounds__(dec::kThreads) __attribute__((amdgpu_num_sgpr(80)))
       };
 
       if (nSeg > 0) loadRaw(nSeg - 1, uint32_t(nSeg - 1) < nFull, rvA);
-      // partial segments: masked steps
+      // partial segments (a pair with an element's tail block, or with no
+      // second block at all): masked steps, unrolled like the full segments
+      // (constant LDS offsets, the ring checked every kUnroll steps); steps
+      // past a block's end are no-ops of the masked step.  A per-step loop
+      // here cost such pairs 7-8 us (1 x 4096 words: decode 33.6 -> 25.7 us)
       for (int32_t g = nSeg - 1; g >= int32_t(nFull); --g) {
-        const int32_t tTop = min(int32_t(T) - 1, g * int32_t(dec::kSegSteps) + int32_t(dec::kSegSteps) - 1);
         const int32_t tBot = g * int32_t(dec::kSegSteps);
-        for (int32_t t = tTop; t >= tBot; --t) {
+#pragma unroll
+        for (int grp = int(dec::kSegSteps / dec::kUnroll) - 1; grp >= 0; --grp) {
 #pragma unroll
           for (int c = 0; c < K; ++c)
 #pragma unroll
             for (int s = 0; s < S; ++s) ringEnsure(st[c][s], lane, kVec);
-          bool vld[K * S];
 #pragma unroll
-          for (int c = 0; c < K; ++c) {
-            const uint32_t uw = lane >= 32 ? uwH[c][1] : uwH[c][0];
+          for (int u = int(dec::kUnroll) - 1; u >= 0; --u) {
+            const int tr = grp * int(dec::kUnroll) + u;
+            const uint32_t t = uint32_t(tBot + tr);
+            bool vld[K * S];
 #pragma unroll
-            for (int s = 0; s < S; ++s) vld[c * S + s] = uint32_t(t) * 32 + l < uw;
+            for (int c = 0; c < K; ++c) {
+              const uint32_t uw = lane >= 32 ? uwH[c][1] : uwH[c][0];
+#pragma unroll
+              for (int s = 0; s < S; ++s) vld[c * S + s] = t * 32 + l < uw;
+            }
+            uint32_t e0[K * S];
+            decStepAll<true, K * S>(chains, vld, lutC, mask, pb, hv, e0);
+#pragma unroll
+            for (int c = 0; c < K; ++c)
+#pragma unroll
+              for (int s = 0; s < S; ++s)
+                if (vld[c * S + s]) segLane[c][s][tr * 32] = uint16_t(e0[c * S + s] >> 16);
           }
-          uint32_t e0[K * S];
-          decStepAll<true, K * S>(chains, vld, lutC, mask, pb, hv, e0);
-#pragma unroll
-          for (int c = 0; c < K; ++c)
-#pragma unroll
-            for (int s = 0; s < S; ++s)
-              if (vld[c * S + s]) segLane[c][s][(t - tBot) * 32] = uint16_t(e0[c * S + s] >> 16);
         }
         __builtin_amdgcn_wave_barrier();
         join(g, false, rvA);

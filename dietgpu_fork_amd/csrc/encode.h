@@ -1163,7 +1163,10 @@ __global__ __launch_bounds__(enc::kThreads) void k_encode(BatchDesc in, BatchDes
       }
       __builtin_amdgcn_wave_barrier();
     }
-    // partial segments (element tail / odd block counts): masked steps
+    // partial segments (element tail / odd block counts): masked steps,
+    // unrolled like the full segments (groups of kUnroll steps, the ring
+    // checked once per group, table reads ahead); steps past a block's end
+    // are no-ops of the masked step
     for (uint32_t g = nFull; g < nSeg; ++g) {
       split(g, false);
 #pragma unroll
@@ -1172,23 +1175,33 @@ __global__ __launch_bounds__(enc::kThreads) void k_encode(BatchDesc in, BatchDes
         for (int s = 0; s < S; ++s) ringFlush<int(R - 256), R>(st[c][s], lane);
       if (g + 1 < nSeg) loadSeg(g + 1);
       __builtin_amdgcn_wave_barrier();
-      const uint32_t tEnd = min(T, (g + 1) * enc::kSegSteps);
-      for (uint32_t t = g * enc::kSegSteps; t < tEnd; ++t) {
+#pragma unroll
+      for (int grp = 0; grp < int(enc::kSegSteps / enc::kUnroll); ++grp) {
 #pragma unroll
         for (int c = 0; c < K; ++c)
 #pragma unroll
-          for (int s = 0; s < S; ++s) ringFlush<int(R - 32), R>(st[c][s], lane);
-        const uint32_t tr = t - g * enc::kSegSteps;
+          for (int s = 0; s < S; ++s) ringFlush<int(R - 128), R>(st[c][s], lane);
+        u32x4 E[enc::kUnroll][K][S];
+        bool vd[enc::kUnroll][K];
 #pragma unroll
-        for (int c = 0; c < K; ++c) {
-          const bool valid = t * 32 + l < uw[c];
+        for (int u = 0; u < int(enc::kUnroll); ++u) {
+          const uint32_t tr = uint32_t(grp * int(enc::kUnroll) + u);
+          const uint32_t t = g * enc::kSegSteps + tr;
 #pragma unroll
-          for (int s = 0; s < S; ++s) {
-            const uint32_t sym = valid ? uint32_t(symLane[c][s][tr * 32]) : 0u;
-            const u32x4 e = tbl[s][sym];
-            encStep<true, R>(st[c][s], valid, e, hv);
+          for (int c = 0; c < K; ++c) {
+            vd[u][c] = t * 32 + l < uw[c];
+#pragma unroll
+            for (int s = 0; s < S; ++s)
+              E[u][c][s] = tbl[s][vd[u][c] ? uint32_t(symLane[c][s][tr * 32]) : 0u];
           }
         }
+#pragma unroll
+        for (int u = 0; u < int(enc::kUnroll); ++u)
+#pragma unroll
+          for (int c = 0; c < K; ++c)
+#pragma unroll
+            for (int s = 0; s < S; ++s) encStep<true, R>(st[c][s], vd[u][c], E[u][c][s], hv);
+        __builtin_amdgcn_sched_barrier(0);
       }
       __builtin_amdgcn_wave_barrier();
     }

@@ -434,7 +434,8 @@ void sparseCompressT(StackDeviceMemory& res, const FloatCompressConfig& config, 
   // compress 85 -> 75 us).  It lengthens every tile's workgroup, so with
   // more elements the separate k_hist over the compacted lists is faster
   // (5 x 15M: 155 us against 170).
-  const bool countHist = nb == 1 && (FT == 4 || !persistentFits(maxN));
+  bool countHist = nb == 1;
+  if constexpr (FT != 4) countHist = countHist && !persistentPreferred<FT>(nb, maxN);
   constexpr int kSegs = FloatTraits<FT>::kSegs;
   // histogram rows: up to 64 per element, accumulated with atomics
   const uint32_t G = tiles;

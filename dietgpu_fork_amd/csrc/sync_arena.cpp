@@ -50,6 +50,9 @@ void setBarrierBudget(uint32_t ticks) { gBarrierBudget.store(ticks); }
 uint32_t barrierBudgetTicks() { return gBarrierBudget.load(); }
 void setDispatchSkew(uint32_t ticks) { gDispatchSkew.store(ticks); }
 uint32_t dispatchSkew() { return gDispatchSkew.load(); }
+std::atomic<int> gCompressPath{0};
+void setCompressPath(int mode) { gCompressPath.store(mode); }
+int compressPath() { return gCompressPath.load(); }
 
 SyncLease::SyncLease(StackDeviceMemory& res, hipStream_t stream, const size_t (&bytesIn)[kSyncRegions],
                      bool dequeue, size_t rowsBytes) {

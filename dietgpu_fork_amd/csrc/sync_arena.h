@@ -104,4 +104,11 @@ uint32_t barrierBudgetTicks();
 void setDispatchSkew(uint32_t ticks);
 uint32_t dispatchSkew();
 
+// Test hook: which compressor takes batches that both can: 0 (default) the
+// size rule (persistentPreferred, codec.hip), 1 the single-pass k_pcompress
+// whenever it can (16 B-aligned elements of at most 1 MiB of symbols, no
+// caller histogram), 2 always the three-kernel path.  Archives are the same.
+void setCompressPath(int mode);
+int compressPath();
+
 }  // namespace dietgpu

@@ -204,6 +204,14 @@ void dietgpu_set_barrier_budget(uint32_t ticks);
  * by dispatched lower workgroups; the single-pass k_pcompress carries no
  * hook, see tools/variants.py pskew).  Archives are unchanged; 0 = off. */
 void dietgpu_set_dispatch_skew(uint32_t ticks);
+/* Test hook: which compressor takes a float / byte batch that both can
+ * compress.  0 (default): the size rule (the single-pass compressor for
+ * batches of more than 256 work items whose teams fit the resident grid,
+ * the three-kernel path below that); 1: the single-pass compressor whenever
+ * the batch is eligible (16 B-aligned inputs, elements of at most 1 MiB of
+ * symbols, no caller histogram); 2: always the three-kernel path.  Archives
+ * are byte-identical whatever the mode; other values mean 0. */
+void dietgpu_set_compress_path(int mode);
 /* Test hook: enqueue on `stream` a kernel of `workgroups` 256-thread
  * workgroups that each hold `lds_bytes` of LDS for `micros` microseconds
  * (<= 1 s) and exit: compute units held by another kernel while the

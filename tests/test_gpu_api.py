@@ -329,19 +329,23 @@ def test_graph_capture_replay(C):
             np.testing.assert_array_equal(arch[i, :ref.size].cpu().numpy(), ref)
 
 
+@pytest.mark.parametrize("path", ["auto", "single-pass", "three-kernel"])
 @pytest.mark.parametrize("sizes", [
     [123457], [123457, 1000], [4095, 65536, 1, 300001],
     [1, 7, 4096, 4097, 8191, 32767, 32768, 32769, 100000, 524287, 524288, 1048576],
     [3000] * 300 + [524288], [12345] * 600,
 ])
-def test_single_pass_shapes(C, ws, sizes):
+def test_single_pass_shapes(C, ws, sizes, path):
     """The persistent single-pass compressor over ragged batches: single
     elements with a partial last item, elements of one item, elements ending
-    inside a block pair, batches of many rounds; bf16 archives identical to
-    the oracle."""
+    inside a block pair, batches of many rounds; and the same batches forced
+    down the three-kernel path (prologue normalisation, masked partial
+    segments) and routed by the size rule; bf16 archives identical to the
+    oracle."""
     g = torch.Generator().manual_seed(len(sizes))
     xs = [torch.randn(n, generator=g).to(torch.bfloat16) for n in sizes]
-    arch, osz = C.float_compress_pointer([x.to(DEV) for x in xs], ws=ws)
+    with C.compress_path(path):
+        arch, osz = C.float_compress_pointer([x.to(DEV) for x in xs], ws=ws)
     got = osz.cpu().tolist()
     host = arch.cpu().numpy()
     for i, x in enumerate(xs):

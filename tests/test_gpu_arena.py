@@ -29,6 +29,15 @@ def env():
     return N, C
 
 
+@pytest.fixture(autouse=True)
+def _single_pass(env):
+    """The aligned batches here are meant for the single-pass compressor
+    (small batches take the three-kernel path by default: the size rule,
+    codec.hip persistentPreferred)."""
+    with env[1].compress_path("single-pass"):
+        yield
+
+
 class Batch:
     """bf16 elements in one device buffer; `aligned` False offsets every
     element by one word (not 16 B-aligned: the fused three-kernel path)."""

@@ -25,6 +25,15 @@ def C():
     return codec
 
 
+@pytest.fixture(autouse=True)
+def _single_pass(C):
+    """Small batches take the three-kernel path by default (the size rule,
+    codec.hip persistentPreferred): this module's batches are meant for the
+    single-pass compressor whenever it can take them."""
+    with C.compress_path("single-pass"):
+        yield
+
+
 @pytest.fixture(scope="module")
 def ws(C):
     return C.Workspace(512 << 20)

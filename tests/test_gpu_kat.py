@@ -3,8 +3,10 @@
 * ANSStatisticsTest.cu:127-149 (Normalization_NonZero: pdf[1] = 2^10 - 255,
   every other symbol 1) and :151-167 (Normalization_EqualWeight: every pdf
   2^10 / 256) encoded by BOTH compressors -- the single-pass k_pcompress
-  (16 B-aligned input) and the three-kernel k_hist -> normalise -> k_encode
-  path (a 1-byte-offset input forces it, as test_gpu_api.py does) -- with the
+  (16 B-aligned input, forced by dietgpu_set_compress_path: one small element
+  takes the three-kernel path by default) and the three-kernel k_hist ->
+  k_encode path (16 B-aligned with its prologue normalisation, and a 1-byte-
+  offset input, as test_gpu_api.py does) -- with the
   archive's pdf table equal to the golden kat_a_pdf / kat_b_pdf and the whole
   archive equal to the oracle's.
 * ANSStatisticsTest.cu:44-95 (Histogram): exact byte histograms of a batch of
@@ -66,13 +68,14 @@ def _on_device(d, offset):
     return big[offset: offset + d.size]
 
 
-@pytest.mark.parametrize("path,offset", [("single_pass", 0), ("three_kernel", 1)])
+@pytest.mark.parametrize("path,offset", [("single-pass", 0), ("three-kernel", 0), ("three-kernel", 1)])
 @pytest.mark.parametrize("name", ["kat_a", "kat_b"])
 def test_normalization_kat(C, ws, G, name, path, offset):
     d = _kat_input(name)
     t = _on_device(d, offset)
-    assert (t.data_ptr() % 16 == 0) == (path == "single_pass")
-    out, sizes = C.ans_encode_pointer([t], prob_bits=10, checksum=False, ws=ws)
+    assert (t.data_ptr() % 16 == 0) == (offset == 0)
+    with C.compress_path(path):
+        out, sizes = C.ans_encode_pointer([t], prob_bits=10, checksum=False, ws=ws)
     arch = out[0, : int(sizes[0])].cpu().numpy()
     pdf = arch[32: 32 + 512].view(np.uint16).astype(np.uint32)  # after the 32 B ANS header
     np.testing.assert_array_equal(pdf, G[name + "_pdf"])

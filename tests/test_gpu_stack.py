@@ -23,6 +23,15 @@ def C():
     return codec
 
 
+@pytest.fixture(autouse=True)
+def _single_pass(C):
+    """Small batches take the three-kernel path by default (the size rule,
+    codec.hip persistentPreferred): this module's batches are meant for the
+    single-pass compressor whenever it can take them."""
+    with C.compress_path("single-pass"):
+        yield
+
+
 def _bf16(n, seed):
     g = torch.Generator().manual_seed(seed)
     return (torch.randn(n, generator=g) * (1 + seed % 3)).to(torch.bfloat16)

@@ -8,7 +8,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 TAG=${TAG:-r4}
 if [ -z "$NOTESTS" ]; then
-  timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread \
+  timeout -k 10 420 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread \
     > gpurun_out/${TAG}_tests.log 2>&1
   tail -2 gpurun_out/${TAG}_tests.log
 fi

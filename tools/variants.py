@@ -237,7 +237,109 @@ DEC2A = [(DH, """      int32_t g = min(nSeg, int32_t(nFull)) - 1;  // rvA holds 
       } else if (g == 0) {
         fullSeg2(0, rvA, rvC);
       }""")]
+# round 5: the decoder's partial (masked) segments unrolled like the full
+# ones -- 8 steps with constant LDS offsets, the ring checked every 4 steps;
+# steps past a block's end are no-ops of the masked step
+DECMASK = [(DH, """      for (int32_t g = nSeg - 1; g >= int32_t(nFull); --g) {
+        const int32_t tTop = min(int32_t(T) - 1, g * int32_t(dec::kSegSteps) + int32_t(dec::kSegSteps) - 1);
+        const int32_t tBot = g * int32_t(dec::kSegSteps);
+        for (int32_t t = tTop; t >= tBot; --t) {
+#pragma unroll
+          for (int c = 0; c < K; ++c)
+#pragma unroll
+            for (int s = 0; s < S; ++s) ringEnsure(st[c][s], lane, kVec);
+          bool vld[K * S];
+#pragma unroll
+          for (int c = 0; c < K; ++c) {
+            const uint32_t uw = lane >= 32 ? uwH[c][1] : uwH[c][0];
+#pragma unroll
+            for (int s = 0; s < S; ++s) vld[c * S + s] = uint32_t(t) * 32 + l < uw;
+          }
+          uint32_t e0[K * S];
+          decStepAll<true, K * S>(chains, vld, lutC, mask, pb, hv, e0);
+#pragma unroll
+          for (int c = 0; c < K; ++c)
+#pragma unroll
+            for (int s = 0; s < S; ++s)
+              if (vld[c * S + s]) segLane[c][s][(t - tBot) * 32] = uint16_t(e0[c * S + s] >> 16);
+        }""", """      for (int32_t g = nSeg - 1; g >= int32_t(nFull); --g) {
+        const int32_t tBot = g * int32_t(dec::kSegSteps);
+#pragma unroll
+        for (int grp = int(dec::kSegSteps / dec::kUnroll) - 1; grp >= 0; --grp) {
+#pragma unroll
+          for (int c = 0; c < K; ++c)
+#pragma unroll
+            for (int s = 0; s < S; ++s) ringEnsure(st[c][s], lane, kVec);
+#pragma unroll
+          for (int u = int(dec::kUnroll) - 1; u >= 0; --u) {
+            const int tr = grp * int(dec::kUnroll) + u;
+            const uint32_t t = uint32_t(tBot + tr);
+            bool vld[K * S];
+#pragma unroll
+            for (int c = 0; c < K; ++c) {
+              const uint32_t uw = lane >= 32 ? uwH[c][1] : uwH[c][0];
+#pragma unroll
+              for (int s = 0; s < S; ++s) vld[c * S + s] = t * 32 + l < uw;
+            }
+            uint32_t e0[K * S];
+            decStepAll<true, K * S>(chains, vld, lutC, mask, pb, hv, e0);
+#pragma unroll
+            for (int c = 0; c < K; ++c)
+#pragma unroll
+              for (int s = 0; s < S; ++s)
+                if (vld[c * S + s]) segLane[c][s][tr * 32] = uint16_t(e0[c * S + s] >> 16);
+          }
+        }""")]
+ENCMASK = [("encode.h", """      const uint32_t tEnd = min(T, (g + 1) * enc::kSegSteps);
+      for (uint32_t t = g * enc::kSegSteps; t < tEnd; ++t) {
+#pragma unroll
+        for (int c = 0; c < K; ++c)
+#pragma unroll
+          for (int s = 0; s < S; ++s) ringFlush<int(R - 32), R>(st[c][s], lane);
+        const uint32_t tr = t - g * enc::kSegSteps;
+#pragma unroll
+        for (int c = 0; c < K; ++c) {
+          const bool valid = t * 32 + l < uw[c];
+#pragma unroll
+          for (int s = 0; s < S; ++s) {
+            const uint32_t sym = valid ? uint32_t(symLane[c][s][tr * 32]) : 0u;
+            const u32x4 e = tbl[s][sym];
+            encStep<true, R>(st[c][s], valid, e, hv);
+          }
+        }
+      }""", """#pragma unroll
+      for (int grp = 0; grp < int(enc::kSegSteps / enc::kUnroll); ++grp) {
+#pragma unroll
+        for (int c = 0; c < K; ++c)
+#pragma unroll
+          for (int s = 0; s < S; ++s) ringFlush<int(R - 128), R>(st[c][s], lane);
+        u32x4 E[enc::kUnroll][K][S];
+        bool vd[enc::kUnroll][K];
+#pragma unroll
+        for (int u = 0; u < int(enc::kUnroll); ++u) {
+          const uint32_t tr = uint32_t(grp * int(enc::kUnroll) + u);
+          const uint32_t t = g * enc::kSegSteps + tr;
+#pragma unroll
+          for (int c = 0; c < K; ++c) {
+            vd[u][c] = t * 32 + l < uw[c];
+#pragma unroll
+            for (int s = 0; s < S; ++s)
+              E[u][c][s] = tbl[s][vd[u][c] ? uint32_t(symLane[c][s][tr * 32]) : 0u];
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < int(enc::kUnroll); ++u)
+#pragma unroll
+          for (int c = 0; c < K; ++c)
+#pragma unroll
+            for (int s = 0; s < S; ++s) encStep<true, R>(st[c][s], vd[u][c], E[u][c][s], hv);
+        __builtin_amdgcn_sched_barrier(0);
+      }""")]
+NOPC = [("codec.hip", "  if (team > pc::kMaxTeam) return false;", "  if (team > 0) return false;")]
 VARS = {
+    "mask2": DECMASK + ENCMASK,
+    "mask2nopc": DECMASK + ENCMASK + NOPC,
+    "decmask": DECMASK,
     "dec2a": DEC2A,
     # the same with the SGPR count held at 80 (84 SGPRs admit 7 workgroups
     # per CU instead of 8, MI355X_MICROARCH.md "Residency")
