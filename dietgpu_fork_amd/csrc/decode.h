@@ -308,7 +308,14 @@ struct Join {
 // 64-bit decode table of one archive: entry[slot] = {pdf | sym << 24,
 // slot - cdf[sym]} (packDecodeLookup, ans/GpuANSDecode.cuh:34-44, re-laid
 // out for v_mad_u32_u24).  scratch: >= 2 * 256 + 4 dwords of LDS.
-__device__ __forceinline__ void buildLut64(gp<const uint16_t> pdfIn, lp<u32x2> lut,
+// Slot-parallel: each thread finds the symbol of its 2^pb / 256 slots by a
+// binary search over the exclusive cdf (the largest s with cdf[s] <= slot,
+// which always has pdf > 0), all of its slots' searches interleaved.  The
+// symbol-parallel fill it replaces (each wave walking 64 symbols in turn)
+// was a chain of 64 dependent LDS round trips: 5.5 of a one-block decode's
+// 25 us.  Slots a corrupt table (pdf sum != 2^pb) leaves uncovered get a
+// neighbouring symbol; none is written outside the table.
+__device__ __forceinline__ void buildLut64(gp<const uint16_t> pdfIn, lp<u32x2> lut, int pb,
                                            uint32_t* scratch) {
   static_assert(dec::kThreads == kNumSymbols, "one symbol per thread");
   uint32_t* cdfS = scratch;
@@ -320,10 +327,28 @@ __device__ __forceinline__ void buildLut64(gp<const uint16_t> pdfIn, lp<u32x2> l
   pdfS[tid] = p;
   cdfS[tid] = c;
   __syncthreads();
-  const uint32_t lane = tid & 63;
-  for (uint32_t s = tid >> 6; s < kNumSymbols; s += dec::kWaves) {
-    const uint32_t ps = pdfS[s], cs = cdfS[s];
-    for (uint32_t j = lane; j < ps; j += 64) lut[cs + j] = u32x2{ps | (s << 24), j};
+  constexpr int kG = 4;  // slots searched together
+  const uint32_t total = 1u << pb;
+#pragma unroll 1
+  for (uint32_t g0 = tid; g0 < total; g0 += kG * dec::kThreads) {
+    uint32_t s[kG], cs[kG];
+#pragma unroll
+    for (int j = 0; j < kG; ++j) s[j] = 0, cs[j] = 0;
+#pragma unroll
+    for (uint32_t bit = kNumSymbols / 2; bit; bit >>= 1) {
+#pragma unroll
+      for (int j = 0; j < kG; ++j) {
+        const uint32_t cv = cdfS[s[j] + bit];
+        const bool up = cv <= g0 + j * dec::kThreads;
+        s[j] = up ? s[j] + bit : s[j];
+        cs[j] = up ? cv : cs[j];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < kG; ++j) {
+      const uint32_t slot = g0 + j * dec::kThreads;
+      if (slot < total) lut[slot] = u32x2{pdfS[s[j]] | (s[j] << 24), slot - cs[j]};
+    }
   }
 }
 
@@ -389,7 +414,7 @@ __global__ __launch_bounds__(dec::kThreads) __attribute__((amdgpu_num_sgpr(80)))
 #pragma unroll
   for (int s = 0; s < S; ++s) {
     buildLut64((gp<const uint16_t>)(arch[s] + kANSHeaderBytes),
-               (lp<u32x2>)(L + s * (lutBytes / S)), (uint32_t*)segAll);
+               (lp<u32x2>)(L + s * (lutBytes / S)), pb, (uint32_t*)segAll);
     __syncthreads();
   }
 

@@ -814,7 +814,7 @@ __device__ __forceinline__ void proNormalize(gp<const uint32_t> rows, uint32_t n
                                              uint16_t (*pdfS)[kNumSymbols]) {
   const uint32_t t = threadIdx.x, q = t & 63, st = t >> 6;
   constexpr uint32_t kPer = kProRows / 4;  // rows per thread (rows congruent to st mod 4)
-  constexpr uint32_t kB = 8;               // loads in flight per segment
+  constexpr uint32_t kB = kPer;            // loads in flight per segment: all (one round trip)
 #pragma unroll
   for (int s = 0; s < S; ++s) {
     gp<const u32x4> p = (gp<const u32x4>)(rows + (uint64_t(s) * nb + b) * kProRows * kNumSymbols) + q;

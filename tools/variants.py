@@ -440,6 +440,27 @@ VARS = {
     "noplace": [(P, "for (uint32_t v = tid; v < nv; v += pc::kThreads) {", "for (uint32_t v = tid; v < nv && nv == 0xFFFFFFFFu; v += pc::kThreads) {")],
     "nosplitst": [(P, "splitVec<FT>(v, i0, it.n, raw, myT + off, myT + off, store);", "splitVec<FT>(v, i0, it.n, raw, myT + off, myT + off, false);")],
 }
+# phase stamps of k_encode (0) / k_decode (1), workgroups 0-63 of element 0,
+# wave 0 (tools/debug/stamp_small.py)
+EH = "encode.h"
+SSTAMP = [
+    ("device.h", "namespace dietgpu {", "namespace dietgpu {\nstatic __device__ unsigned long long g_sstamp[3 * 64 * 16];\n#define SSTAMP(kid, ph) do { if (threadIdx.x == 0 && blockIdx.x < 64 && blockIdx.y == 0) { unsigned long long t_ = __builtin_amdgcn_s_memrealtime(); asm volatile(\"\" : \"+v\"(t_)); ((volatile unsigned long long*)g_sstamp)[((kid) * 64 + blockIdx.x) * 16 + (ph)] = t_; } } while (0)"),
+    (EH, "  const uint32_t wx = blockIdx.x, wy = blockIdx.y;\n  if (kFused && tail.skew", "  SSTAMP(0, 0);\n  const uint32_t wx = blockIdx.x, wy = blockIdx.y;\n  if (kFused && tail.skew"),
+    (EH, "    proNormalize<S>(G(tail.rows), numInBatch, b, n, tail.pb, (lp<u32x4>)&ringS[0][0], tblS, pdfS);\n    __syncthreads();\n", "    proNormalize<S>(G(tail.rows), numInBatch, b, n, tail.pb, (lp<u32x4>)&ringS[0][0], tblS, pdfS);\n    __syncthreads();\n    SSTAMP(0, 1);\n"),
+    (EH, "  if (vecIn)\n    run(std::true_type{});\n  else\n    run(std::false_type{});\n", "  if (vecIn)\n    run(std::true_type{});\n  else\n    run(std::false_type{});\n  SSTAMP(0, 2);\n"),
+    (EH, "    const uint32_t nk = first < nBlocks ? min(uint32_t(Cfg::kBlocksPerWG), nBlocks - first) : 0u;\n", "    const uint32_t nk = first < nBlocks ? min(uint32_t(Cfg::kBlocksPerWG), nBlocks - first) : 0u;\n    SSTAMP(0, 3);\n"),
+    (EH, "      if (lane < nk) preE[lane] = excl + inc - r;\n", "      if (lane < nk) preE[lane] = excl + inc - r;\n      SSTAMP(0, 4);\n"),
+    (EH, "    copyPayload<R>(preE", "    SSTAMP(0, 5);\n    copyPayload<R>(preE"),
+    (EH, "(gp<uint8_t>)(bwords + roundUp(nBlocks, 2)), &ringS[0][0], flE);\n", "(gp<uint8_t>)(bwords + roundUp(nBlocks, 2)), &ringS[0][0], flE);\n    asm volatile(\"s_waitcnt vmcnt(0)\" ::: \"memory\");\n    SSTAMP(0, 6);\n"),
+    (DH, "  gp<const uint8_t> base = startOf(in, b);\n  gp<const uint32_t> fh = (gp<const uint32_t>)base;\n", "  SSTAMP(1, 0);\n  gp<const uint8_t> base = startOf(in, b);\n  gp<const uint32_t> fh = (gp<const uint32_t>)base;\n"),
+    (DH, "#pragma unroll\n  for (int s = 0; s < S; ++s) {\n    buildLut64(", "  SSTAMP(1, 1);\n#pragma unroll\n  for (int s = 0; s < S; ++s) {\n    buildLut64("),
+    (DH, "  const uint32_t w = readfirst(tid >> 6), lane = tid & 63, l = lane & 31;\n  uint32_t hv = lane >= 32", "  SSTAMP(1, 2);\n  const uint32_t w = readfirst(tid >> 6), lane = tid & 63, l = lane & 31;\n  uint32_t hv = lane >= 32"),
+    (DH, "    for (int c = 0; c < K; ++c) T = max(T, max(divUp(uwH[c][0], 32), divUp(uwH[c][1], 32)));\n", "    for (int c = 0; c < K; ++c) T = max(T, max(divUp(uwH[c][0], 32), divUp(uwH[c][1], 32)));\n    SSTAMP(1, 3);\n"),
+    (DH, "      // full segments: unrolled, unmasked\n", "      SSTAMP(1, 4);\n      // full segments: unrolled, unmasked\n"),
+    (DH, "    if (vecIn && vecOut)\n      run(std::true_type{});\n    else\n      run(std::false_type{});\n", "    if (vecIn && vecOut)\n      run(std::true_type{});\n    else\n      run(std::false_type{});\n    asm volatile(\"s_waitcnt vmcnt(0)\" ::: \"memory\");\n    SSTAMP(1, 5);\n"),
+    ("codec.hip", "uint32_t deviceErrorCount(bool reset) {", "extern \"C\" void* dietgpu_debug_sstamps() { void* p = nullptr; (void)hipGetSymbolAddress(&p, HIP_SYMBOL(g_sstamp)); return p; }\n\nuint32_t deviceErrorCount(bool reset) {"),
+]
+VARS["stampsm"] = SSTAMP
 for name in sys.argv[1:]:
     root = f"/tmp/var/{name}"
     shutil.rmtree(root, ignore_errors=True)
