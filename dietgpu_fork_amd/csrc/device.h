@@ -178,35 +178,6 @@ __device__ __forceinline__ uint32_t blockExclusiveScan(uint32_t v, uint32_t* sme
   return before + inc - v;
 }
 
-// rANS decode table in LDS: LUT[s] = (s - cdf[sym]) << 20 | pdf << 8 | sym
-// (packDecodeLookup, ans/GpuANSDecode.cuh:34-44), built by an NT-thread
-// workgroup from the archive's u16 pdf table.
-template <int NT>
-__device__ __forceinline__ void buildLut(gp<const uint16_t> pdfIn, uint32_t* lut, uint32_t* red,
-                                         uint32_t* cdfS, uint32_t* pdfS) {
-  constexpr int kPer = kNumSymbols / NT;  // symbols per thread
-  const uint32_t tid = threadIdx.x;
-  uint32_t p[kPer], sum = 0;
-#pragma unroll
-  for (int k = 0; k < kPer; ++k) {
-    p[k] = pdfIn[tid * kPer + k];
-    sum += p[k];
-  }
-  uint32_t c = blockExclusiveScan<NT>(sum, red, nullptr);
-#pragma unroll
-  for (int k = 0; k < kPer; ++k) {
-    pdfS[tid * kPer + k] = p[k];
-    cdfS[tid * kPer + k] = c;
-    c += p[k];
-  }
-  __syncthreads();
-  const uint32_t lane = tid & 63;
-  for (uint32_t s = tid >> 6; s < kNumSymbols; s += NT / 64) {
-    const uint32_t ps = pdfS[s], cs = cdfS[s];
-    for (uint32_t j = lane; j < ps; j += 64) lut[cs + j] = (j << 20) | (ps << 8) | s;
-  }
-}
-
 // sc1 (agent-scope relaxed) loads / stores: the cross-workgroup hand-offs'
 // accesses (MI355X_MICROARCH.md, sc1 loads in place of an acquire)
 __device__ __forceinline__ uint32_t ldSc1(gp<const uint32_t> p) {

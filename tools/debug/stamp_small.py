@@ -26,11 +26,11 @@ NAMES = {0: ["start", "norm", "steps", "pre-lb", "lookback", "copy", "end"],
 def read():
     torch.cuda.synchronize()
     p = L.dietgpu_debug_sstamps()
-    buf = torch.empty(3 * 64 * 16, dtype=torch.int64, device=dev)
+    buf = torch.empty(3 * 4096 * 16, dtype=torch.int64, device=dev)
     hip = ctypes.CDLL("libamdhip64.so")
     hip.hipMemcpy(ctypes.c_void_p(buf.data_ptr()), ctypes.c_void_p(p), ctypes.c_size_t(buf.numel() * 8), 3)
     torch.cuda.synchronize()
-    return buf.cpu().numpy().reshape(3, 64, 16)
+    return buf.cpu().numpy().reshape(3, 4096, 16)
 
 
 def show(st, kid, nwg):

@@ -346,6 +346,17 @@ VARS = {
     "dec2a80": DEC2A + [(DH, "__global__ __launch_bounds__(dec::kThreads) void k_decode(",
                          "__global__ __launch_bounds__(dec::kThreads) __attribute__((amdgpu_num_sgpr(80))) void k_decode(")],
     "pskew": PSKEW,
+    # decoder output store cache policies (global_store_dwordx4 with the
+    # policy bits in the instruction; "plain" = none)
+    **{f"sp_{name}": [("device.h", """__device__ __forceinline__ void st16nt(gp<void> p, uint4 v) {
+  __builtin_nontemporal_store(u32x4{v.x, v.y, v.z, v.w}, (gp<u32x4>)p);
+}""", """__device__ __forceinline__ void st16nt(gp<void> p, uint4 v) {
+  asm volatile("global_store_dwordx4 %%0, %%1, off %s" :: "v"(p), "v"(u32x4{v.x, v.y, v.z, v.w}) : "memory");
+}""" % pol)] for name, pol in (("plain", ""), ("sc0", "sc0"), ("sc1", "sc1"), ("sc01", "sc0 sc1"),
+                                ("ntsc1", "nt sc1"), ("ntsc0", "nt sc0"), ("nt", "nt"))},
+    # decoder output through plain stores instead of streaming ones
+    "decnont": [("codec.hip", "if (streamOut) return launch(std::integral_constant<int, 0>{}, std::true_type{});",
+                 "if (streamOut) return launch(std::integral_constant<int, 0>{}, std::false_type{});")],
     # VERDICT r4 item 4: a single-read c3 (4 MiB byte elements, teams of
     # 128 items) through k_pcompress, measured instead of extrapolated
     # (timing and archives only; checksummed byte archives would need the
@@ -440,11 +451,12 @@ VARS = {
     "noplace": [(P, "for (uint32_t v = tid; v < nv; v += pc::kThreads) {", "for (uint32_t v = tid; v < nv && nv == 0xFFFFFFFFu; v += pc::kThreads) {")],
     "nosplitst": [(P, "splitVec<FT>(v, i0, it.n, raw, myT + off, myT + off, store);", "splitVec<FT>(v, i0, it.n, raw, myT + off, myT + off, false);")],
 }
-# phase stamps of k_encode (0) / k_decode (1), workgroups 0-63 of element 0,
-# wave 0 (tools/debug/stamp_small.py)
+# phase stamps of k_encode (0) / k_decode (1), the first 4096 workgroups
+# (linear id blockIdx.y * gridDim.x + blockIdx.x), wave 0
+# (tools/debug/stamp_small.py, tools/debug/stamp_dec.py)
 EH = "encode.h"
 SSTAMP = [
-    ("device.h", "namespace dietgpu {", "namespace dietgpu {\nstatic __device__ unsigned long long g_sstamp[3 * 64 * 16];\n#define SSTAMP(kid, ph) do { if (threadIdx.x == 0 && blockIdx.x < 64 && blockIdx.y == 0) { unsigned long long t_ = __builtin_amdgcn_s_memrealtime(); asm volatile(\"\" : \"+v\"(t_)); ((volatile unsigned long long*)g_sstamp)[((kid) * 64 + blockIdx.x) * 16 + (ph)] = t_; } } while (0)"),
+    ("device.h", "namespace dietgpu {", "namespace dietgpu {\nstatic __device__ unsigned long long g_sstamp[3 * 4096 * 16];\n#define SSTAMP(kid, ph) do { const unsigned wg_ = blockIdx.y * gridDim.x + blockIdx.x; if (threadIdx.x == 0 && wg_ < 4096) { unsigned long long t_ = __builtin_amdgcn_s_memrealtime(); asm volatile(\"\" : \"+v\"(t_)); ((volatile unsigned long long*)g_sstamp)[((kid) * 4096 + wg_) * 16 + (ph)] = t_; } } while (0)"),
     (EH, "  const uint32_t wx = blockIdx.x, wy = blockIdx.y;\n  if (kFused && tail.skew", "  SSTAMP(0, 0);\n  const uint32_t wx = blockIdx.x, wy = blockIdx.y;\n  if (kFused && tail.skew"),
     (EH, "    proNormalize<S>(G(tail.rows), numInBatch, b, n, tail.pb, (lp<u32x4>)&ringS[0][0], tblS, pdfS);\n    __syncthreads();\n", "    proNormalize<S>(G(tail.rows), numInBatch, b, n, tail.pb, (lp<u32x4>)&ringS[0][0], tblS, pdfS);\n    __syncthreads();\n    SSTAMP(0, 1);\n"),
     (EH, "  if (vecIn)\n    run(std::true_type{});\n  else\n    run(std::false_type{});\n", "  if (vecIn)\n    run(std::true_type{});\n  else\n    run(std::false_type{});\n  SSTAMP(0, 2);\n"),
@@ -455,12 +467,49 @@ SSTAMP = [
     (DH, "  gp<const uint8_t> base = startOf(in, b);\n  gp<const uint32_t> fh = (gp<const uint32_t>)base;\n", "  SSTAMP(1, 0);\n  gp<const uint8_t> base = startOf(in, b);\n  gp<const uint32_t> fh = (gp<const uint32_t>)base;\n"),
     (DH, "#pragma unroll\n  for (int s = 0; s < S; ++s) {\n    buildLut64(", "  SSTAMP(1, 1);\n#pragma unroll\n  for (int s = 0; s < S; ++s) {\n    buildLut64("),
     (DH, "  const uint32_t w = readfirst(tid >> 6), lane = tid & 63, l = lane & 31;\n  uint32_t hv = lane >= 32", "  SSTAMP(1, 2);\n  const uint32_t w = readfirst(tid >> 6), lane = tid & 63, l = lane & 31;\n  uint32_t hv = lane >= 32"),
-    (DH, "    for (int c = 0; c < K; ++c) T = max(T, max(divUp(uwH[c][0], 32), divUp(uwH[c][1], 32)));\n", "    for (int c = 0; c < K; ++c) T = max(T, max(divUp(uwH[c][0], 32), divUp(uwH[c][1], 32)));\n    SSTAMP(1, 3);\n"),
-    (DH, "      // full segments: unrolled, unmasked\n", "      SSTAMP(1, 4);\n      // full segments: unrolled, unmasked\n"),
-    (DH, "    if (vecIn && vecOut)\n      run(std::true_type{});\n    else\n      run(std::false_type{});\n", "    if (vecIn && vecOut)\n      run(std::true_type{});\n    else\n      run(std::false_type{});\n    asm volatile(\"s_waitcnt vmcnt(0)\" ::: \"memory\");\n    SSTAMP(1, 5);\n"),
+    (DH, "    for (int c = 0; c < K; ++c) T = max(T, max(divUp(uwH[c][0], 32), divUp(uwH[c][1], 32)));\n", "    for (int c = 0; c < K; ++c) T = max(T, max(divUp(uwH[c][0], 32), divUp(uwH[c][1], 32)));\n    SSTAMP(1, 3 + 3 * min(pass, 3u));\n"),
+    (DH, "      // full segments: unrolled, unmasked\n", "      SSTAMP(1, 4 + 3 * min(pass, 3u));\n      // full segments: unrolled, unmasked\n"),
+    (DH, "    if (vecIn && vecOut)\n      run(std::true_type{});\n    else\n      run(std::false_type{});\n", "    if (vecIn && vecOut)\n      run(std::true_type{});\n    else\n      run(std::false_type{});\n    asm volatile(\"s_waitcnt vmcnt(0)\" ::: \"memory\");\n    SSTAMP(1, 5 + 3 * min(pass, 3u));\n"),
     ("codec.hip", "uint32_t deviceErrorCount(bool reset) {", "extern \"C\" void* dietgpu_debug_sstamps() { void* p = nullptr; (void)hipGetSymbolAddress(&p, HIP_SYMBOL(g_sstamp)); return p; }\n\nuint32_t deviceErrorCount(bool reset) {"),
 ]
 VARS["stampsm"] = SSTAMP
+# cost probes (wrong archives): the encode step without its ring write /
+# without the step at all (full segments; table reads kept)
+VARS["noemit"] = [(EH, 'asm volatile("s_and_saveexec_b64 %0, %1\\n\\tds_write_b16', 'if (0) asm volatile("s_and_saveexec_b64 %0, %1\\n\\tds_write_b16')]
+# ring stores without the exec mask: non-writers store to a per-thread
+# discard slot (v_cndmask on the vote), so a step's store no longer orders
+# the next step's VALU behind an exec restore
+TRASH = [
+    (EH, "  gp<uint16_t> out[2];     // per half: slot data\n};",
+     "  gp<uint16_t> out[2];     // per half: slot data\n  uint32_t trash;          // LDS byte address of this thread's discard slot\n};"),
+    (EH, """  uint64_t sav;
+  asm volatile("s_and_saveexec_b64 %0, %1\\n\\tds_write_b16 %2, %3\\n\\ts_mov_b64 exec, %0"
+               : "=&s"(sav)
+               : "s"(vote), "v"(ringAddr), "v"(p.x)
+               : "memory", "scc");""",
+     """  uint32_t wa;
+  asm volatile("v_cndmask_b32_e64 %0, %1, %2, %3\\n\\tds_write_b16 %0, %4"
+               : "=&v"(wa)
+               : "v"(p.trash), "v"(ringAddr), "s"(vote), "v"(p.x)
+               : "memory");"""),
+    (EH, "  __shared__ uint32_t cwE[Cfg::kBlocksPerWG];",
+     "  __shared__ __attribute__((aligned(16))) uint16_t trashS[enc::kThreads];\n  __shared__ uint32_t cwE[Cfg::kBlocksPerWG];"),
+    (EH, "      p.ringLane = p.ring + (hv & R);\n",
+     "      p.ringLane = p.ring + (hv & R);\n      p.trash = uint32_t(size_t((lp<uint16_t>)&trashS[threadIdx.x]));\n"),
+    (P, "  __shared__ __attribute__((aligned(16))) uint16_t rings[pc::kBlocksPerItem * pc::kRing];",
+     "  __shared__ __attribute__((aligned(16))) uint16_t rings[pc::kBlocksPerItem * pc::kRing];\n  __shared__ __attribute__((aligned(16))) uint16_t trashS[pc::kThreads];"),
+    (P, "    p.ringLane = p.ring + (hv & pc::kRing);\n",
+     "    p.ringLane = p.ring + (hv & pc::kRing);\n    p.trash = uint32_t(size_t((lp<uint16_t>)&trashS[threadIdx.x]));\n"),
+]
+VARS["trash"] = TRASH
+VARS["noexec"] = [(EH, 'asm volatile("s_and_saveexec_b64 %0, %1\\n\\tds_write_b16 %2, %3\\n\\ts_mov_b64 exec, %0"',
+                   'asm volatile("s_mov_b64 %0, %1\\n\\tds_write_b16 %2, %3"')]
+VARS["noidx"] = [(EH, "const uint32_t ringAddr = uint32_t(size_t(p.ringLane + (idx & (kRing - 1))));",
+                  "(void)idx; const uint32_t ringAddr = uint32_t(size_t(p.ringLane + (__builtin_amdgcn_mbcnt_lo(~0u, 0u) & 31)));")]
+VARS["nostep"] = [(EH, "for (int s = 0; s < S; ++s) encStep<false, R>(st[c][s], true, E[u][c][s], hv);",
+                   "for (int s = 0; s < S; ++s) st[c][s].x += E[u][c][s].z;"),
+                  (P, "for (uint32_t u = 0; u < enc::kUnroll; ++u) encStep<false, pc::kRing>(p, true, Ev[u], hv);",
+                   "for (uint32_t u = 0; u < enc::kUnroll; ++u) p.x += Ev[u].z;")]
 for name in sys.argv[1:]:
     root = f"/tmp/var/{name}"
     shutil.rmtree(root, ignore_errors=True)
