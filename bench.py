@@ -575,9 +575,12 @@ def _bf16_trunc(nb, words, seed, dev):
 def _extras_small_batches(dev, pb, record, breakdown):
     """batches whose single-pass teams were not
     XCD-aligned before round 5 (1-7 multi-item elements; 33 x 1e6 words,
-    whose teams cannot be aligned within the resident grid), with the
-    compressor's team-barrier fallback count over every timed call (must be
-    0: a fallback means a hand-off that waited out the 200 us budget)."""
+    whose teams cannot be aligned within the resident grid).  Timed as the
+    library routes them (the size rule sends all four to the three-kernel
+    path, csrc/codec.hip persistentPreferred), and once more forced through
+    the single-pass compressor (dietgpu_set_compress_path) with its
+    team-barrier fallback count over every timed call (must be 0: a
+    fallback means a hand-off that waited out the 200 us budget)."""
     import torch
 
     from dietgpu_fork_amd import codec as C
@@ -587,19 +590,26 @@ def _extras_small_batches(dev, pb, record, breakdown):
         ws = C.Workspace(1 << 30, dev)
         arch, sizes = C.float_compress_stride(x, prob_bits=pb, ws=ws)
         y, ok, _ = C.float_decompress_stride(arch, words, torch.bfloat16, prob_bits=pb, ws=ws)
-        C.barrier_fallback_count(reset=True)
         tc = _timed(lambda: C.float_compress_stride(x, prob_bits=pb, ws=ws, out=arch, sizes=sizes), 3,
                     max_reps=400)
+        ref = arch.clone()
+        C.barrier_fallback_count(reset=True)
+        with C.compress_path("single-pass"):
+            tc_sp = _timed(lambda: C.float_compress_stride(x, prob_bits=pb, ws=ws, out=arch, sizes=sizes), 3,
+                           max_reps=400)
         fb = C.barrier_fallback_count(reset=True)
+        same = torch.equal(arch, ref)
+        del ref
         td = _timed(lambda: C.float_decompress_stride(arch, words, torch.bfloat16, prob_bits=pb, ws=ws, out=y), 3,
                     max_reps=400)
         exact = bool((ok == 1).all()) and torch.equal(x.view(torch.int16), y.view(torch.int16))
         kern = breakdown(lambda: C.float_compress_stride(x, prob_bits=pb, ws=ws, out=arch, sizes=sizes),
                          lambda: C.float_decompress_stride(arch, words, torch.bfloat16, prob_bits=pb, ws=ws,
                                                            out=y))
-        record(f"small batch {nb} x {words} bf16 N(0,1) (floatCompress stride; single-pass team layout)",
-               x.numel() * 2, int(sizes.to(torch.int64).sum()), tc, td, exact, kernels_ms=kern,
-               barrier_fallbacks=fb)
+        record(f"small batch {nb} x {words} bf16 N(0,1) (floatCompress stride; size-rule path, "
+               f"single-pass forced for the fallback count)",
+               x.numel() * 2, int(sizes.to(torch.int64).sum()), tc, td, exact and same, kernels_ms=kern,
+               single_pass_compress_ms=round(tc_sp, 4), barrier_fallbacks=fb)
         del x, y, arch, ws
     torch.cuda.empty_cache()
     return []

@@ -6,8 +6,10 @@ tools/ablibs/<name>.so (git-ignored); tools/ab.sh (c2 bench),
 tools/debug/extras_ab.sh (secondary configs) and tools/debug/sp_ab.sh
 (sparse) swap them in on the GPU box.  The variants below are the round-2
 experiments recorded in DESIGN.md section 7; a substitution that no longer
-matches the current sources fails loudly.
-    usage: python tools/variants.py name..."""
+matches the current sources fails loudly (earlier rounds' variants whose
+anchors are gone stay here as the record of what was measured; --check
+lists which still apply).
+    usage: python tools/variants.py name...  |  python tools/variants.py --check"""
 import os, shutil, subprocess, sys
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 P = "pcompress.h"
@@ -510,6 +512,12 @@ VARS["nostep"] = [(EH, "for (int s = 0; s < S; ++s) encStep<false, R>(st[c][s], 
                    "for (int s = 0; s < S; ++s) st[c][s].x += E[u][c][s].z;"),
                   (P, "for (uint32_t u = 0; u < enc::kUnroll; ++u) encStep<false, pc::kRing>(p, true, Ev[u], hv);",
                    "for (uint32_t u = 0; u < enc::kUnroll; ++u) p.x += Ev[u].z;")]
+if sys.argv[1:] == ["--check"]:
+    for name, subs in VARS.items():
+        live = all(os.path.exists(f"{REPO}/dietgpu_fork_amd/csrc/{f}") and
+                   open(f"{REPO}/dietgpu_fork_amd/csrc/{f}").read().count(a) >= 1 for f, a, _ in subs)
+        print(f"{name:32s} {'applies' if live else 'stale (anchors gone)'}")
+    sys.exit(0)
 for name in sys.argv[1:]:
     root = f"/tmp/var/{name}"
     shutil.rmtree(root, ignore_errors=True)
