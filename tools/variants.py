@@ -504,6 +504,26 @@ TRASH = [
      "    p.ringLane = p.ring + (hv & pc::kRing);\n    p.trash = uint32_t(size_t((lp<uint16_t>)&trashS[threadIdx.x]));\n"),
 ]
 VARS["trash"] = TRASH
+# k_sparseExpand writing each lane's word straight from the list gather
+# (coalesced 4 B stores per step) instead of staging the tile in LDS
+SPX = "sparse.hip"
+EXPD_TAIL = (SPX, """  gp<W> y = (gp<W>)out.start(b);
+#pragma unroll
+  for (uint32_t t = 0; t < kT; ++t) {
+    const uint32_t t0 = (tile0 + t) * kTileWords;
+    if (t0 >= n) break;""", """  gp<W> y = (gp<W>)out.start(b);
+#pragma unroll
+  for (uint32_t t = 0; t < kT; ++t) {
+    const uint32_t t0 = (tile0 + t) * kTileWords;
+    if (t0 >= n || t0 < n) break;""")
+# cost probes (wrong output): no tile prefix / no list gather in k_sparseExpand
+VARS["expnopre"] = [(SPX, "  uint32_t pos = tilePrefix(G(tileCounts) + uint64_t(b) * tilesPerElem, tile0, red);",
+                     "  uint32_t pos = 0; (void)red;")]
+VARS["expnogather"] = [(SPX, "      buf[t][q] = f ? list[src] : W(0);", "      buf[t][q] = f ? W(src) : W(0);")]
+VARS["expdirect"] = [(SPX, "      buf[t][q] = f ? list[src] : W(0);",
+                      "      if (i < n) ((gp<W>)out.start(b))[i] = f ? list[src] : W(0);"), EXPD_TAIL]
+VARS["expdirectnt"] = [(SPX, "      buf[t][q] = f ? list[src] : W(0);",
+                        "      if (i < n) __builtin_nontemporal_store(f ? list[src] : W(0), (gp<W>)out.start(b) + i);"), EXPD_TAIL]
 VARS["noexec"] = [(EH, 'asm volatile("s_and_saveexec_b64 %0, %1\\n\\tds_write_b16 %2, %3\\n\\ts_mov_b64 exec, %0"',
                    'asm volatile("s_mov_b64 %0, %1\\n\\tds_write_b16 %2, %3"')]
 VARS["noidx"] = [(EH, "const uint32_t ringAddr = uint32_t(size_t(p.ringLane + (idx & (kRing - 1))));",
