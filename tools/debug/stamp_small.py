@@ -43,15 +43,18 @@ def show(st, kid, nwg):
             print(f"   wg {w:3d}: " + " ".join(f"{v:7.2f}" for v in rel[w]))
 
 
+FP64 = os.environ.get("FP64")  # c4's fp64 tensor instead (16 M words)
 SHAPES = [(1, 4096), (1, 1000000), (8, 1000000)]
 if len(sys.argv) > 1:
     SHAPES = [tuple(int(v) for v in s.split("x")) for s in sys.argv[1:]]
 for nb, n in SHAPES:
     g = torch.Generator(device=dev).manual_seed(nb + n)
-    x = (torch.randn(nb, n, generator=g, device=dev).view(torch.int32) >> 16).to(torch.int16).view(torch.bfloat16)
+    dt = torch.float64 if FP64 else torch.bfloat16
+    x = (torch.randn(nb, n, generator=g, device=dev, dtype=torch.float64) if FP64 else
+         (torch.randn(nb, n, generator=g, device=dev).view(torch.int32) >> 16).to(torch.int16).view(torch.bfloat16))
     ws = C.Workspace(512 << 20, dev)
     arch, sizes = C.float_compress_stride(x, ws=ws)
-    y, ok, _ = C.float_decompress_stride(arch, n, torch.bfloat16, ws=ws)
+    y, ok, _ = C.float_decompress_stride(arch, n, dt, ws=ws)
     for _ in range(20):
         C.float_compress_stride(x, ws=ws, out=arch, sizes=sizes)
     st = read()
@@ -59,7 +62,7 @@ for nb, n in SHAPES:
     nwgE = min(64, -(-n // (4096 * 8)))
     show(st, 0, max(1, nwgE))
     for _ in range(20):
-        C.float_decompress_stride(arch, n, torch.bfloat16, ws=ws, out=y)
+        C.float_decompress_stride(arch, n, dt, ws=ws, out=y)
     st = read()
     nwgD = min(64, -(-n // (4096 * 8)))
     show(st, 1, max(1, nwgD))
