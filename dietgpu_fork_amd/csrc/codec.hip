@@ -484,10 +484,10 @@ void encodeBatchDevice(StackDeviceMemory& res, int pb, bool useChecksum, uint32_
     }
     if (!kFused) {
       prof::Scope p("coalesce", s);
-      // blocks per workgroup: 8 (c4 fp64: 1,024 workgroups for the two
+      // blocks per workgroup: 4 (c4 fp64: 2,048 workgroups for the two
       // segments' 4,096 blocks each; 32 gave 256 and a latency-bound copy:
-      // coalesce 28.4 -> 16 us, same box)
-      const uint32_t bpw = 8;
+      // coalesce 28.4 -> 16 us at 8, 15.0 at 4, 19.2 at 16, same box)
+      const uint32_t bpw = 4;
       dim3 g(std::max(1u, divUp(MB, bpw)), ny, kSegs);
       k_coalesce<FT><<<g, kThreads, 0, s>>>(in, out, y0, nb, std::max(MB, 1u), bpw, slots.data(),
                                             cw.data(), pdf, pb, useChecksum, ck.data(),

@@ -520,6 +520,9 @@ EXPD_TAIL = (SPX, """  gp<W> y = (gp<W>)out.start(b);
 VARS["expnopre"] = [(SPX, "  uint32_t pos = tilePrefix(G(tileCounts) + uint64_t(b) * tilesPerElem, tile0, red);",
                      "  uint32_t pos = 0; (void)red;")]
 VARS["expnogather"] = [(SPX, "      buf[t][q] = f ? list[src] : W(0);", "      buf[t][q] = f ? W(src) : W(0);")]
+# fp64 k_coalesce granularity (blocks per workgroup; 4 is the product's)
+VARS["bpw8"] = [("codec.hip", "      const uint32_t bpw = 4;", "      const uint32_t bpw = 8;")]
+VARS["bpw16"] = [("codec.hip", "      const uint32_t bpw = 4;", "      const uint32_t bpw = 16;")]
 VARS["expdirect"] = [(SPX, "      buf[t][q] = f ? list[src] : W(0);",
                       "      if (i < n) ((gp<W>)out.start(b))[i] = f ? list[src] : W(0);"), EXPD_TAIL]
 VARS["expdirectnt"] = [(SPX, "      buf[t][q] = f ? list[src] : W(0);",
