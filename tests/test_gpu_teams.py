@@ -116,3 +116,29 @@ def test_fallback_counter_counts(C, ws):
     for i, w in enumerate(words):
         ref = O.float_compress(w, 2)
         np.testing.assert_array_equal(host[i, : ref.size], ref)
+
+
+def test_size_rule_routes_by_work_items(C, ws):
+    """The size rule (codec.hip persistentPreferred): with
+    the barrier budget at 0 every single-pass team of more than 16 items
+    falls back, so the fallback counter shows which compressor ran.  3 x 1e6
+    words (93 items) go to the three-kernel path by default (no fallback)
+    and single-pass when forced; 16 x 1e6 (496 items, XCD-aligned) stay
+    single-pass by default.  Archives are the oracle's either way."""
+    cases = ((3, "auto", False), (3, "single-pass", True), (16, "auto", True))
+    for nb, mode, single in cases:
+        words, x = _bf16_batch(nb, 1000000, seed0=91 + nb)
+        C.barrier_fallback_count(reset=True)
+        try:
+            C.set_barrier_budget(0)
+            with C.compress_path(mode):
+                out, sizes = C.float_compress_stride(x, prob_bits=10, ws=ws)
+            torch.cuda.synchronize()
+        finally:
+            C.set_barrier_budget(20000)
+        assert (C.barrier_fallback_count(reset=True) > 0) == single, (nb, mode)
+        assert C.device_error_count(reset=True) == 0
+        host = out.cpu().numpy()
+        for i in (0, nb - 1):
+            ref = O.float_compress(words[i], 2)
+            np.testing.assert_array_equal(host[i, : ref.size], ref, err_msg=f"{nb} {mode} element {i}")
