@@ -74,7 +74,11 @@ def main():
         raise SystemExit("--gpus > 1 must be launched with torch.distributed.run (one rank/GPU)")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    # launched by torch.distributed.run (WORLD_SIZE set), world 1 included:
+    # the multi-GPU step runs as is -- RCCL process group, the size all-gather
+    # inside every step, barriers and max-over-ranks timing
+    distributed = "WORLD_SIZE" in os.environ
+    if distributed:
         dist.init_process_group("nccl", device_id=dev)
 
     n, pb = args.words, args.prob_bits
@@ -117,7 +121,7 @@ def main():
     def step():
         N.check(L.dietgpu_float_compress(ws.h, ft, pb, 0, nb, in_ptrs, in_size, comp_ptrs,
                                          sizes.data_ptr(), stream))
-        if world > 1:  # the only exchange: per-element compressed sizes (RCCL)
+        if distributed:  # the only exchange: per-element compressed sizes (RCCL)
             D.gather_sizes(sizes, total)
         N.check(L.dietgpu_float_decompress(ws.h, ft, pb, 0, nb, comp_ptrs, out_ptrs, caps,
                                            ok.data_ptr(), osz.data_ptr(), stream))
@@ -161,7 +165,7 @@ def main():
     torch.cuda.synchronize()
     per_step = (time.perf_counter() - t_s) / 8
     settle_steps = max(0, int(args.settle_ms * 1e-3 / max(per_step, 1e-6)) - 8)
-    if world > 1:
+    if distributed:
         c = torch.tensor([settle_steps], dtype=torch.int64, device=dev)
         dist.all_reduce(c, op=dist.ReduceOp.MAX)
         settle_steps = int(c.item())
@@ -177,14 +181,14 @@ def main():
     C.profile_reset()
     C.profile_filter(dominant)
     C.profile(not args.no_kernel_events and dominant is not None)
-    if world > 1:
+    if distributed:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
     torch.cuda.synchronize()
-    if world > 1:
+    if distributed:
         dist.barrier()
     t1 = time.perf_counter()
     C.profile(False)
@@ -214,7 +218,7 @@ def main():
         torch.cuda.synchronize()
         assert torch.equal(out.view(torch.int16), x.view(torch.int16)), "roundtrip mismatch (cold decode)"
     elapsed = t1 - t0
-    if world > 1:
+    if distributed:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
@@ -252,6 +256,7 @@ def main():
         "higher_is_better": True,
         "scaling": "strong" if workload == "c5" else "weak", "vs_baseline": None, "dtype": "u32",
         "data": "synthetic",
+        "distributed": distributed,
         "config": {"workload": (f"c5: batch={total} x {n * 2 // 1048576} MiB bf16 N(0,1) in total, "
                                 f"{nb} per GPU" if workload == "c5" else
                                 f"c2: batch={nb} x {n * 2 // 1048576} MiB bf16 N(0,1) per GPU"),
@@ -290,7 +295,7 @@ def main():
         line["extras"] = _extras(dev, pb)
     if rank == 0:
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if distributed:
         dist.destroy_process_group()
 
 
@@ -551,6 +556,8 @@ def _extras(dev, pb, reps=3):
     out.extend(_extras_small_batches(dev, pb, record, breakdown))
     out.extend(_extras_batch1_sweep(dev, pb, record, breakdown))
     out.extend(_extras_reference_grid(dev))
+    out.append(_extras_float_benchmark_grid(dev))
+    out.append(_extras_sparse_benchmark_grid(dev))
     out.append(_extras_c5_g1(dev, pb))
     return out
 
@@ -717,6 +724,103 @@ def _extras_reference_grid(dev):
     del tmp
     torch.cuda.empty_cache()
     return res
+
+
+FT_OF = {"float16": 1, "bfloat16": 2, "float32": 3, "float64": 4}
+INT_OF = {2: "int16", 4: "int32", 8: "int64"}
+
+
+def _grid_row(ft_name, nb, words, U, Cb, tc, td, exact, **kw):
+    """One compact row of a benchmark grid: whole-call times (back-to-back
+    calls, events on the launch stream), the reference's GB/s (U / t), and
+    the call's HBM roofline 2(U + C) / (t_c + t_d) against 8 TB/s."""
+    call = 2 * (U + Cb) / ((tc + td) * 1e-3) / 1e9
+    return {"type": ft_name, "batch": nb, "words": words, "ratio": round(Cb / U, 5),
+            "compress_ms": round(tc, 4), "decompress_ms": round(td, 4),
+            "compress_GBps": round(U / tc / 1e6, 1), "decompress_GBps": round(U / td / 1e6, 1),
+            "call_GBps": round(call, 1), "call_frac": round(call / HBM_PEAK_GBPS, 4),
+            "roundtrip_bit_exact": bool(exact), **kw}
+
+
+def _extras_float_benchmark_grid(dev):
+    """The fork's own float_benchmark (FloatBenchmark.cu:401-427, README.md:20):
+    fp16 / bf16 / fp32 / fp64, batch 1 x {1e5, 1.5e5, 1e6, 1.5e6, 1e7, 1.5e7,
+    1e8} N(0,1) words, pb 9, floatCompress / floatDecompress pointer API
+    (FloatBenchmark.cu:224-273).  Each point: bit-exact roundtrip check and
+    whole-call roofline."""
+    import torch
+
+    from dietgpu_fork_amd import codec as C
+
+    rows = []
+    ws = C.Workspace(2 << 30, dev)
+    for name, dt in (("float16", torch.float16), ("bfloat16", torch.bfloat16), ("float32", torch.float32),
+                     ("float64", torch.float64)):
+        for words in (100000, 150000, 1000000, 1500000, 10000000, 15000000, 100000000):
+            g = torch.Generator(device=dev).manual_seed(10 + words)
+            x = torch.randn(words, generator=g, device=dev, dtype=torch.float64 if dt == torch.float64
+                            else torch.float32).to(dt)
+            arch, sizes = C.float_compress_pointer([x], prob_bits=9, ws=ws)
+            row = [arch[0]]
+            y = torch.empty_like(x)
+            ok, _ = C.float_decompress_pointer(row, [y], prob_bits=9, ws=ws)
+            iv = getattr(torch, INT_OF[x.element_size()])
+            exact = int(ok[0]) == 1 and torch.equal(x.view(iv), y.view(iv))
+            reps = 3 if words >= 1e7 else 10
+            tc = _timed(lambda: C.float_compress_pointer([x], prob_bits=9, ws=ws), reps, max_reps=400)
+            td = _timed(lambda: C.float_decompress_pointer(row, [y], prob_bits=9, ws=ws), reps, max_reps=400)
+            rows.append(_grid_row(name, 1, words, x.numel() * x.element_size(), int(sizes[0]), tc, td, exact))
+            del x, y, arch, row
+        torch.cuda.empty_cache()
+    del ws
+    torch.cuda.empty_cache()
+    return {"config": "float_benchmark grid (FloatBenchmark.cu:421-427): 4 float types x batch 1 x "
+                      "{1e5 .. 1e8} N(0,1) words, pb 9, floatCompress / floatDecompress pointer API",
+            "rows": rows}
+
+
+def _extras_sparse_benchmark_grid(dev):
+    """The fork's sparse_float_benchmark (SparseFloatBenchmark.cu:395-447):
+    fp16 / bf16 / fp32 / fp64 x batch {1, 3, 5} x {1e5, 1.5e5, 1e6, 1.5e6,
+    1e7, 1.5e7} words per element, 50 % zeros (generateSparseFloats'
+    default), N(0,1) nonzeros, pb 9, sparse compress / decompress.  Each
+    point: bit-exact roundtrip check and whole-call roofline (U = the dense
+    input bytes, as the reference's GB/s counts them)."""
+    import torch
+
+    from dietgpu_fork_amd import codec as C
+
+    rows = []
+    ws = C.Workspace(2 << 30, dev)
+    for name, dt in (("float16", torch.float16), ("bfloat16", torch.bfloat16), ("float32", torch.float32),
+                     ("float64", torch.float64)):
+        for nbs in (1, 3, 5):
+            for words in (100000, 150000, 1000000, 1500000, 10000000, 15000000):
+                g = torch.Generator(device=dev).manual_seed(10 + nbs * words)
+                fs = []
+                for _ in range(nbs):
+                    f = torch.randn(words, generator=g, device=dev,
+                                    dtype=torch.float64 if dt == torch.float64 else torch.float32).to(dt)
+                    f[torch.rand(words, generator=g, device=dev) < 0.5] = 0
+                    fs.append(f)
+                arch, sizes = C.sparse_compress(fs, prob_bits=9, ws=ws)
+                ys = [torch.empty_like(f) for f in fs]
+                rws = [arch[i, : int(sizes[i])] for i in range(nbs)]
+                ok, _ = C.sparse_decompress(rws, ys, prob_bits=9, ws=ws)
+                iv = getattr(torch, INT_OF[fs[0].element_size()])
+                exact = bool((ok == 1).all()) and all(torch.equal(a.view(iv), b.view(iv)) for a, b in zip(fs, ys))
+                reps = 3 if words >= 1e7 else 10
+                tc = _timed(lambda: C.sparse_compress(fs, prob_bits=9, ws=ws), reps, max_reps=400)
+                td = _timed(lambda: C.sparse_decompress(rws, ys, prob_bits=9, ws=ws), reps, max_reps=400)
+                rows.append(_grid_row(name, nbs, words, nbs * words * fs[0].element_size(),
+                                      int(sizes.to(torch.int64).sum()), tc, td, exact))
+                del fs, ys, arch, rws
+            torch.cuda.empty_cache()
+    del ws
+    torch.cuda.empty_cache()
+    return {"config": "sparse_float_benchmark grid (SparseFloatBenchmark.cu:440-447): 4 float types x batch "
+                      "{1, 3, 5} x {1e5 .. 1.5e7} words, 50 % zeros, pb 9, sparse compress / decompress",
+            "rows": rows}
 
 
 def _extras_c5_g1(dev, pb, steps=10):

@@ -6,7 +6,8 @@ sparse float codec, behind the reference's C++ API (include/dietgpu/*.h), a
 C ABI (include/dietgpu_c.h, libdietgpu_amd.so) and the ``torch.ops.dietgpu``
 operator surface (dietgpu/DietGpu.cpp).
 
-``import dietgpu_fork_amd`` registers ``torch.ops.dietgpu.*``.
+``import dietgpu_fork_amd`` registers ``torch.ops.dietgpu.*`` and raises
+ImportError when libdietgpu_amd.so or libdietgpu_torch.so is not built.
 """
 from . import _native  # noqa: F401
 from ._native import ChecksumMismatch, DietGpuError, build  # noqa: F401
@@ -22,7 +23,6 @@ def load_library():
     ops.register()
 
 
-try:  # register on import when the HIP library is present
-    load_library()
-except ImportError:
-    pass
+# register on import: a missing HIP or operator library raises ImportError
+# here (there is no CPU fallback; build with __graft_entry__.build())
+load_library()

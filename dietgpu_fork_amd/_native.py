@@ -42,8 +42,6 @@ def _declare(L):
         "dietgpu_set_barrier_budget": (None, [c_u32]),
         "dietgpu_set_dispatch_skew": (None, [c_u32]),
         "dietgpu_set_compress_path": (None, [c_int]),
-        "dietgpu_test_occupy": (c_int, [P, c_u32, c_u32, c_u32]),
-        "dietgpu_test_histogram": (c_int, [vp, c_u32, P, c_u32, c_u32, P, P]),
         "dietgpu_version": (ctypes.c_char_p, []),
         "dietgpu_stack_create": (vp, [c_int, P, c_size]),
         "dietgpu_stack_destroy": (None, [vp]),
@@ -87,7 +85,7 @@ def _declare(L):
                                           ctypes.POINTER(ctypes.c_uint64)]),
     }
     # test hooks absent from older builds (same-box A/B of earlier libraries)
-    optional = {"dietgpu_set_barrier_budget", "dietgpu_set_dispatch_skew", "dietgpu_test_occupy", "dietgpu_test_histogram",
+    optional = {"dietgpu_set_barrier_budget", "dietgpu_set_dispatch_skew",
                 "dietgpu_barrier_fallback_count", "dietgpu_set_compress_path"}
     for name, (res, args) in sig.items():
         if name in optional and not hasattr(L, name):
@@ -100,6 +98,37 @@ def _declare(L):
 
 EXPORTED = None
 _lib = None
+TESTLIB_PATH = os.path.join(_HERE, "_lib", "libdietgpu_testhooks.so")
+TEST_EXPORTED = None
+_testlib = None
+
+
+def testlib():
+    """The test-hook library (include/dietgpu_testhooks.h): GPU tests only,
+    never loaded by the package itself."""
+    global _testlib, TEST_EXPORTED
+    if _testlib is None:
+        lib()
+        if not os.path.exists(TESTLIB_PATH):
+            raise ImportError(f"dietgpu_fork_amd: test-hook library not built ({TESTLIB_PATH})")
+        T = ctypes.CDLL(TESTLIB_PATH, mode=ctypes.RTLD_GLOBAL)
+        c_u32, c_int, P = ctypes.c_uint32, ctypes.c_int, ctypes.c_void_p
+        sig = {"dietgpu_test_last_error": (ctypes.c_char_p, []),
+               "dietgpu_test_occupy": (c_int, [P, c_u32, c_u32, c_u32]),
+               "dietgpu_test_histogram": (c_int, [P, c_u32, P, c_u32, c_u32, P, P])}
+        for name, (res, args) in sig.items():
+            f = getattr(T, name)
+            f.restype = res
+            f.argtypes = args
+        TEST_EXPORTED = sorted(sig)
+        _testlib = T
+    return _testlib
+
+
+def test_check(rc):
+    """check() for the test-hook library's return codes."""
+    if rc != DIETGPU_OK:
+        raise DietGpuError(testlib().dietgpu_test_last_error().decode(errors="replace"))
 
 
 def lib():

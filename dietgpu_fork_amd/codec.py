@@ -37,13 +37,13 @@ def _ws(ws, device):
 
 
 def test_histogram(x2d, size=None, ws=None):
-    """Test hook: per-row byte histograms of a [nb, stride] uint8 CUDA tensor
+    """Test hook (libdietgpu_testhooks.so): per-row byte histograms of a [nb, stride] uint8 CUDA tensor
     (the first `size` bytes of each row) by the compressor's histogram kernel."""
     nb, stride = x2d.shape
     size = stride if size is None else size
     hist = torch.empty([nb, 256], dtype=torch.int32, device=x2d.device)
     ws = _ws(ws, x2d.device)
-    N.check(N.lib().dietgpu_test_histogram(ws.h, nb, x2d.data_ptr(), size, stride, hist.data_ptr(), _s()))
+    N.test_check(N.testlib().dietgpu_test_histogram(ws.h, nb, x2d.data_ptr(), size, stride, hist.data_ptr(), _s()))
     return hist
 
 

@@ -17,7 +17,7 @@ namespace dietgpu {
 #define DG_CONST __attribute__((address_space(4)))
 
 // Per-call pointer / size / offset tables small enough to ride in the kernel
-// arguments of the hot kernels (k_compress, k_decode): the reference inlines
+// arguments of the hot kernels (k_pcompress, k_decode): the reference inlines
 // up to 128 pointers in its kernel parameters (BatchProviderInlinePointer,
 // ans/BatchProvider.cuh:100-194); here up to 8 KB of table (about 400
 // elements), so a pointer-API call launches no upload kernel at all.

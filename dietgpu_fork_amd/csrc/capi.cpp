@@ -15,15 +15,7 @@
 
 using namespace dietgpu;
 
-namespace dietgpu {
-void testOccupy(hipStream_t s, uint32_t micros, uint32_t workgroups, uint32_t ldsBytes);
-void testHistogram(StackDeviceMemory& res, hipStream_t s, uint32_t nb, const void* in_dev, uint32_t size,
-                   uint32_t stride, uint32_t* hist_dev);
-}
-
-struct dietgpu_stack {
-  StackDeviceMemory* mem;
-};
+#include "capi_internal.h"
 
 namespace {
 thread_local std::string gLastError;
@@ -321,21 +313,6 @@ void dietgpu_set_spin_cap(uint32_t polls) { setSpinCap(polls); }
 void dietgpu_set_barrier_budget(uint32_t ticks) { setBarrierBudget(ticks); }
 void dietgpu_set_dispatch_skew(uint32_t ticks) { setDispatchSkew(ticks); }
 void dietgpu_set_compress_path(int mode) { setCompressPath(mode < 0 || mode > 2 ? 0 : mode); }
-
-int dietgpu_test_occupy(void* stream, uint32_t micros, uint32_t workgroups, uint32_t lds_bytes) {
-  return guarded([&] {
-    testOccupy(S(stream), micros, workgroups, lds_bytes);
-    return DIETGPU_OK;
-  });
-}
-
-int dietgpu_test_histogram(dietgpu_stack* res, uint32_t nb, const void* in_dev, uint32_t size,
-                           uint32_t stride, uint32_t* hist_dev, void* stream) {
-  return guarded([&] {
-    testHistogram(R(res), S(stream), nb, in_dev, size, stride, hist_dev);
-    return DIETGPU_OK;
-  });
-}
 
 void dietgpu_profile_enable(int on) { prof::setEnabled(on != 0); }
 void dietgpu_profile_filter(const char* kernel) { prof::setFilter(kernel); }

@@ -82,7 +82,7 @@ void checkProbBits(int pb) {
 // parameter tables (the reference's BatchProvider pointer / size arrays)
 // ---------------------------------------------------------------------------
 // Small tables (allowInline, <= 8 KB) ride in the InlineTable kernel argument
-// of k_compress / k_decode: the BatchDesc fields then hold byte offsets into
+// of k_pcompress / k_decode: the BatchDesc fields then hold byte offsets into
 // it (biased by 8, so none is 0) and BatchDesc::inl says which.  Any other
 // kernel gets a device copy made in its driver's scope (DeviceDescs).  Larger
 // tables, or callers that need device pointers, get one upload here.
@@ -369,12 +369,16 @@ void encodeBatchDevice(StackDeviceMemory& res, int pb, bool useChecksum, uint32_
 
   // Prologue normalisation (k_encode<.., kPro>, encode.h proNormalize):
   // when the encode grid is at most two generations of resident workgroups,
-  // k_hist accumulates kProRows rows per (segment, element) with atomics (in
-  // the sync arena) and every encode workgroup normalises its element
-  // itself, instead of a k_histReduce / k_normalize launch.  Not for byte
-  // archives with a checksum (their partial checksums are summed by the
-  // normalisation kernels) nor for caller-supplied histograms.
-  const bool pro = runHist && !userHist && !rawCk && MB > 0 &&
+  // k_hist accumulates P = proRowsOf(chunks) rows per (segment, element) with
+  // atomics (in the sync arena) and every encode workgroup normalises its
+  // element itself, instead of a k_histReduce / k_normalize launch.  Not for
+  // byte archives with a checksum (their partial checksums are summed by the
+  // normalisation kernels) nor for caller-supplied histograms, and only while
+  // the rows (double-buffered in the stream's arena, which never shrinks)
+  // stay within kProRowsBudget.
+  constexpr size_t kProRowsBudget = 32ull << 20;
+  const size_t proRowsBytes = size_t(kSegs) * nb * proRowsOf(chunks) * kNumSymbols * 4;
+  const bool pro = runHist && !userHist && !rawCk && MB > 0 && proRowsBytes <= kProRowsBudget &&
                    uint64_t(nb) * nW <= 2ull * residentSlots(reinterpret_cast<const void*>(&k_encode<FT, 0, true>),
                                                              enc::kThreads, 0);
   auto partHist = res.alloc<uint32_t>(s, runHist && !pro ? size_t(kSegs) * nb * chunks * kNumSymbols : 1);
@@ -404,7 +408,7 @@ void encodeBatchDevice(StackDeviceMemory& res, int pb, bool useChecksum, uint32_
   // workgroup, epoch-tagged, never zeroed), the last-arrival counters and
   // (pro) the histogram rows, in this stream's sync arena
   const size_t regions[kSyncRegions] = {0, kFused ? size_t(nb) * nW * 8 : 0, 0, 0, size_t(nb) * kSegs * 4, 0};
-  SyncLease lease(res, s, regions, false, pro ? size_t(kSegs) * nb * kProRows * kNumSymbols * 4 : 0);
+  SyncLease lease(res, s, regions, false, pro ? proRowsBytes : 0);
   NormArgs na;
   na.in = in;
   na.hist = userHist ? hist_dev : (reduce2 ? groupHist.data() : chunkRows);
@@ -473,6 +477,7 @@ void encodeBatchDevice(StackDeviceMemory& res, int pb, bool useChecksum, uint32_
       tail.skew = dispatchSkew();
       if (pro) {
         tail.rows = static_cast<const uint32_t*>(lease.rows[0]);
+        tail.rowsPer = proRowsOf(chunks);
         tail.pdfOut = pdfMem.data();
         k_encode<FT, 0, true><<<g, enc::kThreads, 0, s>>>(in, out, y0, nb, std::max(MB, 1u), table,
                                                           slots.data(), cw.data(), tail);

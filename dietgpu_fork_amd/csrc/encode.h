@@ -317,12 +317,15 @@ static __global__ __launch_bounds__(kThreads) void k_normalize(NormArgs a, uint3
 // ---------------------------------------------------------------------------
 constexpr int kHistCols = 32;
 // kRows (small three-kernel grids, k_encode's prologue normalisation):
-// chunk c adds its counts with atomics into row c % kProRows of
-// [segs][nb][kProRows][256] (this call's zeroed buffer of the sync arena),
-// so the encoder sums kProRows rows instead of a k_histReduce / k_normalize
-// launch summing thousands; zero bins add nothing.  `zeroNext`: the same
-// layout in the other buffer, zeroed here for the next call (SyncLease::rows).
+// chunk c adds its counts with atomics into row c % P of [segs][nb][P][256],
+// P = proRowsOf(chunks) = min(chunks, kProRows) (this call's zeroed buffer of
+// the sync arena), so the encoder sums P rows instead of a k_histReduce /
+// k_normalize launch summing thousands; zero bins add nothing.  Sized by the
+// chunk count, so a batch of many one-chunk elements holds one row per
+// element and segment, not 64.  `zeroNext`: the same layout in the other
+// buffer, zeroed here for the next call (SyncLease::rows).
 constexpr uint32_t kProRows = 64;
+__host__ __device__ constexpr uint32_t proRowsOf(uint32_t chunks) { return chunks < kProRows ? chunks : kProRows; }
 
 template <int FT, bool kChecksum, bool kRows = false>
 __global__ __launch_bounds__(kThreads) void k_hist(BatchDesc in, uint32_t batchOffset,
@@ -423,11 +426,11 @@ __global__ __launch_bounds__(kThreads) void k_hist(BatchDesc in, uint32_t batchO
 #pragma unroll
     for (int k = 0; k < kHistCols; ++k) sum += hs[s][tid * kHistCols + ((k + tid) & (kHistCols - 1))];
     if constexpr (kRows) {
-      const uint64_t row = (uint64_t(s) * numInBatch + b) * kProRows + (c & (kProRows - 1));
+      const uint32_t P = proRowsOf(chunksPerElem);
+      const uint64_t row = (uint64_t(s) * numInBatch + b) * P + c % P;
       if (sum) __hip_atomic_fetch_add(G(partHist) + row * kNumSymbols + tid, sum, __ATOMIC_RELAXED,
                                       __HIP_MEMORY_SCOPE_AGENT);
-      for (uint32_t r = c; r < kProRows; r += chunksPerElem)
-        G(zeroNext)[((uint64_t(s) * numInBatch + b) * kProRows + r) * kNumSymbols + tid] = 0;
+      if (c < P) G(zeroNext)[row * kNumSymbols + tid] = 0;
     } else {
       gp<uint32_t> dst = G(partHist) + ((uint64_t(s) * numInBatch + b) * chunksPerElem + c) * kNumSymbols + tid;
       if (na.arrive) stSc1(dst, sum);  // read by this launch's last arrival
@@ -792,15 +795,16 @@ struct EncTail {
   const uint32_t* sparseN = nullptr;
   uint32_t skew = 0;  // test hook: emulated out-of-order start (skewDelay, device.h)
   uint32_t epoch = 0;  // this call's epoch: the flags are epoch-tagged (sync arena), never zeroed
-  // prologue normalisation (k_encode<.., kPro>): k_hist's kProRows rows per
-  // (segment, element), and (fp64) where workgroup 0 leaves the pdf rows for
-  // k_coalesce
+  // prologue normalisation (k_encode<.., kPro>): k_hist's rowsPer
+  // (proRowsOf(chunks)) rows per (segment, element), and (fp64) where
+  // workgroup 0 leaves the pdf rows for k_coalesce
   const uint32_t* rows = nullptr;
+  uint32_t rowsPer = kProRows;
   uint16_t* pdfOut = nullptr;
 };
 
 // Prologue normalisation of k_encode (small grids): every workgroup sums its
-// element's kProRows histogram rows per segment (k_hist<.., kRows>) and
+// element's P <= kProRows histogram rows per segment (k_hist<.., kRows>) and
 // normalises them itself -- wave s segment s, in registers (normalizeWave)
 // -- into its LDS encode table and pdf row.  The redundant work is a few
 // microseconds at the start of a one-generation grid; the k_histReduce /
@@ -809,24 +813,23 @@ struct EncTail {
 // batch-1 float tensors).  red4: S * 256 16 B scratch.  Whole workgroup;
 // the caller synchronises before reading tblS / pdfS.
 template <int S>
-__device__ __forceinline__ void proNormalize(gp<const uint32_t> rows, uint32_t nb, uint32_t b, uint32_t n,
-                                             int pb, lp<u32x4> red4, uint32_t (*tblS)[kNumSymbols * 4],
-                                             uint16_t (*pdfS)[kNumSymbols]) {
+__device__ __forceinline__ void proNormalize(gp<const uint32_t> rows, uint32_t P, uint32_t nb, uint32_t b,
+                                             uint32_t n, int pb, lp<u32x4> red4,
+                                             uint32_t (*tblS)[kNumSymbols * 4], uint16_t (*pdfS)[kNumSymbols]) {
   const uint32_t t = threadIdx.x, q = t & 63, st = t >> 6;
   constexpr uint32_t kPer = kProRows / 4;  // rows per thread (rows congruent to st mod 4)
-  constexpr uint32_t kB = kPer;            // loads in flight per segment: all (one round trip)
 #pragma unroll
   for (int s = 0; s < S; ++s) {
-    gp<const u32x4> p = (gp<const u32x4>)(rows + (uint64_t(s) * nb + b) * kProRows * kNumSymbols) + q;
+    gp<const u32x4> p = (gp<const u32x4>)(rows + (uint64_t(s) * nb + b) * P * kNumSymbols) + q;
+    // every row of this thread in flight at once (one round trip); rows past
+    // P (wave-uniform) are not loaded
+    u32x4 v[kPer];
+#pragma unroll
+    for (uint32_t k = 0; k < kPer; ++k)
+      v[k] = st + 4 * k < P ? p[uint64_t(st + 4 * k) * (kNumSymbols / 4)] : u32x4{0, 0, 0, 0};
     u32x4 acc = u32x4{0, 0, 0, 0};
 #pragma unroll
-    for (uint32_t k0 = 0; k0 < kPer; k0 += kB) {
-      u32x4 v[kB];
-#pragma unroll
-      for (uint32_t k = 0; k < kB; ++k) v[k] = p[uint64_t(st + 4 * (k0 + k)) * (kNumSymbols / 4)];
-#pragma unroll
-      for (uint32_t k = 0; k < kB; ++k) acc += v[k];
-    }
+    for (uint32_t k = 0; k < kPer; ++k) acc += v[k];
     red4[s * kThreads + st * 64 + q] = acc;
   }
   __syncthreads();
@@ -1017,7 +1020,7 @@ __global__ __launch_bounds__(enc::kThreads) void k_encode(BatchDesc in, BatchDes
   gp<uint8_t> states = o + kANSHeaderBytes + kPdfBytes;
   gp<uint2> bwords = (gp<uint2>)(states + uint64_t(kStateBytesPerBlock) * nBlocks);
   if constexpr (kPro) {
-    proNormalize<S>(G(tail.rows), numInBatch, b, n, tail.pb, (lp<u32x4>)&ringS[0][0], tblS, pdfS);
+    proNormalize<S>(G(tail.rows), tail.rowsPer, numInBatch, b, n, tail.pb, (lp<u32x4>)&ringS[0][0], tblS, pdfS);
     __syncthreads();
     if (!kFused && wx == 0) {
 #pragma unroll

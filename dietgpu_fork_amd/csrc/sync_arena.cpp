@@ -1,4 +1,5 @@
-// Per-(device, stream) flag arenas for k_compress (see sync_arena.h).
+// Per-(device, stream) sync arenas of the compressors (k_pcompress, k_encode;
+// see sync_arena.h).
 #include "sync_arena.h"
 
 #include <algorithm>

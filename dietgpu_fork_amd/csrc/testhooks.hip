@@ -1,4 +1,6 @@
-// Test hooks (not part of the reference API): a bounded-duration kernel that
+// Test-hook library libdietgpu_testhooks.so (include/dietgpu_testhooks.h; not
+// linked into the product library).  Not part of the reference API: a
+// bounded-duration kernel that
 // holds compute units, so tests can run the compressor while another kernel
 // occupies part of the chip (pcompress.h, "Forward progress"); and the byte
 // histogram of the three-kernel compressor's first pass exposed on its own,
@@ -8,8 +10,13 @@
 #include <algorithm>
 #include <cstdint>
 
+#include <exception>
+#include <string>
+
+#include "capi_internal.h"
 #include "common.h"
 #include "dietgpu/StackDeviceMemory.h"
+#include "dietgpu_testhooks.h"
 #include "encode.h"
 
 namespace dietgpu {
@@ -69,3 +76,39 @@ void testOccupy(hipStream_t s, uint32_t micros, uint32_t workgroups, uint32_t ld
 }
 
 }  // namespace dietgpu
+
+namespace {
+thread_local std::string gTestError;
+
+template <typename F>
+int guardedTest(F&& f) {
+  try {
+    gTestError.clear();
+    f();
+    return DIETGPU_OK;
+  } catch (const std::exception& e) {
+    gTestError = e.what();
+  } catch (...) {
+    gTestError = "unknown error";
+  }
+  return DIETGPU_ERR_INVALID;
+}
+}  // namespace
+
+extern "C" {
+
+const char* dietgpu_test_last_error(void) { return gTestError.c_str(); }
+
+int dietgpu_test_occupy(void* stream, uint32_t micros, uint32_t workgroups, uint32_t lds_bytes) {
+  return guardedTest([&] { dietgpu::testOccupy(reinterpret_cast<hipStream_t>(stream), micros, workgroups, lds_bytes); });
+}
+
+int dietgpu_test_histogram(dietgpu_stack* res, uint32_t nb, const void* in_dev, uint32_t size,
+                           uint32_t stride, uint32_t* hist_dev, void* stream) {
+  return guardedTest([&] {
+    DG_CHECK(res && res->mem, "null dietgpu_stack");
+    dietgpu::testHistogram(*res->mem, reinterpret_cast<hipStream_t>(stream), nb, in_dev, size, stride, hist_dev);
+  });
+}
+
+}  // extern "C"

@@ -42,7 +42,7 @@ def archive_offsets(sizes, align=16):
 
 class GpuFloatCodec:
     """The float codec on the local GPU (ops.compress_data /
-    ops.decompress_data: k_compress, k_decode) for the compressed collectives."""
+    ops.decompress_data: k_pcompress or k_hist -> k_encode, then k_decode) for the compressed collectives."""
 
     def __init__(self, checksum=False):
         self.checksum = checksum

@@ -205,25 +205,17 @@ void dietgpu_set_barrier_budget(uint32_t ticks);
  * hook, see tools/variants.py pskew).  Archives are unchanged; 0 = off. */
 void dietgpu_set_dispatch_skew(uint32_t ticks);
 /* Test hook: which compressor takes a float / byte batch that both can
- * compress.  0 (default): the size rule (the single-pass compressor for
- * batches of more than 256 work items whose teams fit the resident grid,
- * the three-kernel path below that); 1: the single-pass compressor whenever
+ * compress.  0 (default): the size rule (csrc/codec.hip persistentPreferred;
+ * INTEGRATION.md, "Which compressor runs"): a batch goes to the three-kernel
+ * path when it has at most 256 work items (elements x 8-block items per
+ * element) or when it fits one round of teams that cannot be XCD-aligned,
+ * and to the single-pass compressor otherwise; byte archives with a
+ * checksum always go single-pass (the three-kernel path has no prologue
+ * normalisation for them) unless mode 2 is set; 1: the single-pass compressor whenever
  * the batch is eligible (16 B-aligned inputs, elements of at most 1 MiB of
  * symbols, no caller histogram); 2: always the three-kernel path.  Archives
  * are byte-identical whatever the mode; other values mean 0. */
 void dietgpu_set_compress_path(int mode);
-/* Test hook: enqueue on `stream` a kernel of `workgroups` 256-thread
- * workgroups that each hold `lds_bytes` of LDS for `micros` microseconds
- * (<= 1 s) and exit: compute units held by another kernel while the
- * compressor runs. */
-int dietgpu_test_occupy(void* stream, uint32_t micros, uint32_t workgroups, uint32_t lds_bytes);
-/* Test hook: hist_dev[b * 256 + s] = count of byte value s in element b of a
- * stride batch (nb <= 65535 elements of `size` bytes, `stride` bytes apart),
- * computed by the compressor's own histogram kernel.  Replaces the
- * reference's ansHistogramBatch as its ANSStatisticsTest.cu:44-95 calls it
- * (ans/GpuANSStatistics.cuh:113-143). */
-int dietgpu_test_histogram(dietgpu_stack* res, uint32_t nb, const void* in_dev, uint32_t size,
-                           uint32_t stride, uint32_t* hist_dev, void* stream);
 
 #ifdef __cplusplus
 }

@@ -45,8 +45,8 @@ def N():
     return _native
 
 
-def declared_functions():
-    text = open(HEADER).read()
+def declared_functions(header=HEADER):
+    text = open(header).read()
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
     return sorted(set(re.findall(r"\b(dietgpu_[a-z0-9_]+)\s*\(", text)))
 
@@ -66,6 +66,20 @@ def test_library_exports_every_declared_symbol(N):
     assert not missing, missing
     # and the Python binding declares a signature for each of them
     assert sorted(N.EXPORTED) == declared_functions()
+
+
+def test_test_hooks_live_in_their_own_library(N):
+    """The test-only kernels are not in the product library: they are built
+    into libdietgpu_testhooks.so (include/dietgpu_testhooks.h), which the GPU
+    tests load beside it."""
+    L = N.lib()
+    hdr = os.path.join(ROOT, "include", "dietgpu_testhooks.h")
+    hooks = [f for f in declared_functions(hdr) if f.startswith("dietgpu_test_")]
+    assert hooks and all(not hasattr(L, f) for f in hooks)
+    assert not any(f.startswith("dietgpu_test_") for f in declared_functions())
+    T = N.testlib()
+    assert all(hasattr(T, f) for f in hooks)
+    assert N.TEST_EXPORTED == hooks
 
 
 def test_host_queries_match_reference(N):
@@ -168,3 +182,18 @@ def test_cpp_api_program_links():
     assert os.path.exists(exe)
     r = subprocess.run([exe], capture_output=True, text=True, timeout=60)
     assert r.returncode in (0, 2), r.stderr
+
+
+def test_import_raises_without_the_library(tmp_path):
+    """No silent fallback: a package copy whose HIP libraries are not built
+    fails at `import dietgpu_fork_amd` (Boundary)."""
+    import shutil
+    import subprocess
+    import sys
+
+    shutil.copytree(os.path.join(ROOT, "dietgpu_fork_amd"), tmp_path / "dietgpu_fork_amd",
+                    ignore=shutil.ignore_patterns("_lib", "csrc", "__pycache__"))
+    r = subprocess.run([sys.executable, "-c", "import dietgpu_fork_amd"], cwd=tmp_path,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0
+    assert "ImportError" in r.stderr and "not built" in r.stderr, r.stderr[-2000:]

@@ -148,3 +148,37 @@ def test_prenormalised_sparse_after_single_pass(env):
             assert int(sizes[0]) == ref.size
             np.testing.assert_array_equal(out[0, : ref.size].cpu().numpy(), ref, err_msg=f"round {k}")
     assert C.device_error_count(reset=True) == 0
+
+
+def test_three_kernel_rows_back_to_back(env):
+    """Consecutive three-kernel calls on one stream whose prologue-
+    normalisation rows change shape call to call: the rows of a
+    call are [segments][nb][min(chunks, 64)] in one of the arena's two
+    buffers, and each call's k_hist zeroes the other buffer for the next
+    call, so every layout below reads rows the previous (different) layout
+    zeroed.  Chunk counts 1, 2, 3, 5 and > 64, one and two segments (fp64),
+    batch sizes 1 to 200; every archive (sentinel-filled output) must equal
+    the oracle's."""
+    N, C = env
+    ws = C.Workspace(256 << 20)
+    s = torch.cuda.Stream()
+    cases = [(2, 1, 1_000_000), (3, 3, 12_000), (4, 200, 3_000), (2, 1, 8_192), (1, 16, 20_000),
+             (4, 2, 300_000), (2, 1, 1_000_000), (3, 3, 12_000), (4, 200, 3_000), (1, 64, 4_096)]
+    tdt = {1: torch.int16, 2: torch.int16, 3: torch.int32, 4: torch.int64}
+    ndt = {1: np.int16, 2: np.int16, 3: np.int32, 4: np.int64}
+    C.device_error_count(reset=True)
+    with C.compress_path("three-kernel"), torch.cuda.stream(s):
+        for k, (ft, nb, n) in enumerate(cases):
+            words = [float_words(ft, n, seed=1000 * k + i) for i in range(nb)]
+            x = torch.from_numpy(np.stack(words).view(ndt[ft])).to(DEV)
+            cols = C.max_float_compressed_size(ft, n)
+            out = torch.full([nb, cols], SENTINEL, dtype=torch.uint8, device=DEV)
+            sizes = torch.empty([nb], dtype=torch.int32, device=DEV)
+            C.float_compress_stride(x.view(tdt[ft]), ft=ft, ws=ws, out=out, sizes=sizes)
+            s.synchronize()
+            host, sz = out.cpu().numpy(), sizes.cpu().tolist()
+            for i, w in enumerate(words):
+                ref = O.float_compress(w, ft)
+                assert sz[i] == ref.size, (k, i, sz[i], ref.size)
+                np.testing.assert_array_equal(host[i, : ref.size], ref, err_msg=f"call {k} element {i}")
+    assert C.device_error_count(reset=True) == 0

@@ -1,6 +1,6 @@
 """Compressed collectives (dietgpu_fork_amd/dist.py) over RCCL on one GPU:
-world_size 1 with the "nccl" backend runs the real GPU codec (k_compress,
-k_decode) and the real RCCL calls; the gloo world-2 test in test_dist.py
+world_size 1 with the "nccl" backend runs the real GPU codec (k_pcompress or
+k_hist -> k_encode, k_decode) and the real RCCL calls; the gloo world-2 test in test_dist.py
 covers the multi-rank bookkeeping on the CPU."""
 import socket
 

@@ -1,9 +1,10 @@
 """GPU parity of the two compression paths (csrc/codec.hip encodeBatchDevice):
-the single-pass k_compress (teams of at most cmp::kMaxTeam = 32 workgroups,
+the single-pass k_pcompress (teams of at most pc::kMaxTeam = 32 workgroups,
 i.e. elements of at most 1 MiB of ANS symbols) and the three-kernel
-k_hist -> k_normalize -> k_encode path taken above that.  Both must write the
+k_hist -> k_encode path (k_normalize / k_histReduce, or the encoder's
+prologue normalisation) taken otherwise.  Both must write the
 oracle's archive byte for byte, including dense blocks whose output spills
-out of k_compress's 1024-word LDS rings and blocks that emit no words."""
+out of the 1024-word LDS rings and blocks that emit no words."""
 import numpy as np
 import pytest
 import torch
@@ -90,7 +91,8 @@ def test_constant_input_emits_no_words(C, ws):
 
 @pytest.mark.parametrize("offset_words", [1, 3])
 def test_float_unaligned_input(C, ws, offset_words):
-    """Input not 16 B aligned: k_compress's scalar split path."""
+    """Input not 16 B aligned: the three-kernel path (k_pcompress reads whole
+    16 B vectors, so the host routes unaligned inputs to k_hist -> k_encode)."""
     g = torch.Generator().manual_seed(offset_words)
     base = torch.randn(70000 + offset_words, generator=g).to(torch.bfloat16)
     x = base[offset_words:]

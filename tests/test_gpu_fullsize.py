@@ -112,3 +112,38 @@ def test_batch1_1e9_bf16(C):
     out, ok, osz = C.float_decompress_stride(arch, n, torch.bfloat16, prob_bits=10, ws=ws)
     assert bool((ok == 1).all()) and int(osz[0]) == n
     assert torch.equal(out.view(torch.int16), x.view(torch.int16))
+
+
+def test_fp64_1e8_float_benchmark_point(C):
+    """The largest dense point of the fork's own float_benchmark
+    (FloatBenchmark.cu:421-427: batch 1 x 1e8 fp64 words, pb 9, floatCompress
+    pointer API, N(0,1)): the two-pass fp64 archive is byte-identical to the
+    serial oracle's (the whole 1e8-word element, not a sample), its header
+    reads back through floatGetCompressedInfo, and the roundtrip is exact."""
+    import ctypes
+
+    from dietgpu_fork_amd import _native as N
+
+    n = 100_000_000
+    g = torch.Generator(device=DEV).manual_seed(108)
+    x = torch.randn(n, generator=g, device=DEV, dtype=torch.float64)
+    ws = C.Workspace(3 << 30)
+    arch, sizes = C.float_compress_pointer([x], prob_bits=9, ws=ws)
+    s = int(sizes[0])
+    assert 0 < s <= arch.shape[1] and s % 16 == 0
+    assert C.device_error_count(reset=True) == 0
+    ref = O.float_compress(x.view(torch.int64).cpu().numpy().view(np.uint64), 4, 9)
+    assert s == ref.size
+    np.testing.assert_array_equal(arch[0, :s].cpu().numpy(), ref)
+    del ref
+    sz = torch.zeros([1], dtype=torch.int32, device=DEV)
+    ty = torch.zeros([1], dtype=torch.int32, device=DEV)
+    ck = torch.zeros([1], dtype=torch.int32, device=DEV)
+    N.check(N.lib().dietgpu_float_get_compressed_info(ws.h, N.ptr_array([arch[0].data_ptr()]), 1, sz.data_ptr(),
+                                                      ty.data_ptr(), ck.data_ptr(),
+                                                      ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)))
+    assert int(sz[0]) == n and int(ty[0]) == 4
+    y = torch.empty_like(x)
+    ok, osz = C.float_decompress_pointer([arch[0, :s]], [y], prob_bits=9, ws=ws)
+    assert int(ok[0]) == 1 and int(osz[0]) == n
+    assert torch.equal(y.view(torch.int64), x.view(torch.int64))

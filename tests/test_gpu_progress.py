@@ -99,8 +99,7 @@ def test_compress_beside_occupying_kernel(C, ws):
     C.device_error_count(reset=True)
     side = torch.cuda.Stream()
     torch.cuda.synchronize()
-    rc = N.lib().dietgpu_test_occupy(ctypes.c_void_p(side.cuda_stream), 30000, 256, 80 * 1024)
-    assert rc == 0, N.lib().dietgpu_last_error()
+    N.test_check(N.testlib().dietgpu_test_occupy(ctypes.c_void_p(side.cuda_stream), 30000, 256, 80 * 1024))
     out, sizes = C.float_compress_stride(x, prob_bits=10, ws=ws)
     torch.cuda.synchronize()
     assert C.device_error_count(reset=True) == 0

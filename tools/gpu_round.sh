@@ -8,7 +8,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 TAG=${TAG:-r4}
 if [ -z "$NOTESTS" ]; then
-  timeout -k 10 420 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread \
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
     > gpurun_out/${TAG}_tests.log 2>&1
   tail -2 gpurun_out/${TAG}_tests.log
 fi
@@ -17,6 +17,6 @@ if [ -n "$AB" ]; then
   cat gpurun_out/${TAG}_ab.txt
 fi
 if [ -z "$NOBENCH" ]; then
-  timeout -k 10 400 python bench.py $BENCH_ARGS > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.err
+  timeout -k 10 600 python bench.py $BENCH_ARGS > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.err
   head -c 600 gpurun_out/${TAG}_bench.json
 fi
