@@ -5,7 +5,7 @@ roundtrip bit for bit, then runs `reps` compress + decompress calls
 back to back and prints whole-call times (events on the launch stream).
     usage: python tools/debug/shape_prof.py SHAPE [reps]
 SHAPE: c3 | raw_bf16_b | raw_bf16_nb | raw_fp32_b | fp64_16m | fp64_1e8 |
-       sp_fp64_5x15m | sp_fp32_5x15m | sp_fp32_1x15m90 | c2"""
+       sp_fp64_5x15m | sp_fp32_5x15m | sp_fp32_1x15m90 | c2 | c5 | bf16_1e9"""
 import os
 import sys
 
@@ -77,6 +77,20 @@ def build(shape, ws):
         return (lambda: C.sparse_compress(fs, prob_bits=9, ws=ws),
                 lambda: C.sparse_decompress(rows, ys, prob_bits=9, ws=ws),
                 lambda: all(torch.equal(a.view(iv), b.view(iv)) for a, b in zip(fs, ys)))
+    if shape in ("c5", "bf16_1e9"):
+        nb, n = (8192, 524288) if shape == "c5" else (1, 1070000000)
+        x = torch.empty([nb, n], dtype=torch.bfloat16, device=DEV)
+        g = torch.Generator(device=DEV).manual_seed(5)
+        flat = x.view(-1)
+        for i in range(0, flat.numel(), 1 << 28):
+            m = min(1 << 28, flat.numel() - i)
+            flat[i:i + m] = (torch.randn(m, generator=g, device=DEV).view(torch.int32) >> 16).to(
+                torch.int16).view(torch.bfloat16)
+        arch, sizes = C.float_compress_stride(x, ws=ws)
+        y = torch.empty_like(x)
+        return (lambda: C.float_compress_stride(x, ws=ws, out=arch, sizes=sizes),
+                lambda: C.float_decompress_stride(arch, n, torch.bfloat16, ws=ws, out=y),
+                lambda: torch.equal(x.view(torch.int16), y.view(torch.int16)))
     if shape == "c2":
         g = torch.Generator(device=DEV).manual_seed(0)
         x32 = torch.randn(256, 524288, generator=g, device=DEV)

@@ -475,6 +475,13 @@ SSTAMP = [
     ("codec.hip", "uint32_t deviceErrorCount(bool reset) {", "extern \"C\" void* dietgpu_debug_sstamps() { void* p = nullptr; (void)hipGetSymbolAddress(&p, HIP_SYMBOL(g_sstamp)); return p; }\n\nuint32_t deviceErrorCount(bool reset) {"),
 ]
 VARS["stampsm"] = SSTAMP
+# round 6: half of each CU's dispatch slots start `ticks` late, so their
+# hand-off windows fall in the other slots' segment phases
+def STHALF(ticks):
+    return [(P, "  if (iL >= A().items) return;\n", "  if (iL >= A().items) return;\n  if (blockIdx.x / A().slotSpan >= 2) {\n    const unsigned long long t0_ = __builtin_amdgcn_s_memrealtime();\n    while (__builtin_amdgcn_s_memrealtime() - t0_ < %dull) __builtin_amdgcn_s_sleep(8);\n  }\n" % ticks)]
+VARS["sth5"] = STHALF(500)
+VARS["sth10"] = STHALF(1000)
+VARS["sth15"] = STHALF(1500)
 # cost probes (wrong archives): the encode step without its ring write /
 # without the step at all (full segments; table reads kept)
 VARS["noemit"] = [(EH, 'asm volatile("s_and_saveexec_b64 %0, %1\\n\\tds_write_b16', 'if (0) asm volatile("s_and_saveexec_b64 %0, %1\\n\\tds_write_b16')]
