@@ -404,10 +404,11 @@ void encodeBatchDevice(StackDeviceMemory& res, int pb, bool useChecksum, uint32_
   // launch (c3 hist 0.74 -> 1.09 ms), so k_normalize runs there.
   const bool finalInReduce = reduce2;
   const bool finalInHist = !reduce2 && !pro && runHist && uint64_t(chunks) * nb <= 4096;
-  // k_encode's look-back flags (fused formats: one per element and encode
-  // workgroup, epoch-tagged, never zeroed), the last-arrival counters and
-  // (pro) the histogram rows, in this stream's sync arena
-  const size_t regions[kSyncRegions] = {0, kFused ? size_t(nb) * nW * 8 : 0, 0, 0, size_t(nb) * kSegs * 4, 0};
+  // k_encode's look-back flags (one per segment, element and encode
+  // workgroup, epoch-tagged, never zeroed; fp64's end as the prefixes
+  // k_coalesce reads), the last-arrival counters and (pro) the histogram
+  // rows, in this stream's sync arena
+  const size_t regions[kSyncRegions] = {0, size_t(kSegs) * nb * nW * 8, 0, 0, size_t(nb) * kSegs * 4, 0};
   SyncLease lease(res, s, regions, false, pro ? proRowsBytes : 0);
   NormArgs na;
   na.in = in;
@@ -470,9 +471,8 @@ void encodeBatchDevice(StackDeviceMemory& res, int pb, bool useChecksum, uint32_
     if (MB > 0 || kFused) {
       prof::Scope p("encode", s);
       dim3 g(nW, ny);
-      EncTail tail{pdf, ck.data(), outSize_dev,
-                   kFused ? static_cast<uint64_t*>(lease.base[kSyncFlags]) : nullptr, nW, pb, useChecksum,
-                   spinCap(), deviceErrorWord(), sparseN};
+      EncTail tail{pdf, ck.data(), outSize_dev, static_cast<uint64_t*>(lease.base[kSyncFlags]), nW, pb,
+                   useChecksum, spinCap(), deviceErrorWord(), sparseN};
       tail.epoch = lease.epoch;
       tail.skew = dispatchSkew();
       if (pro) {
@@ -494,9 +494,15 @@ void encodeBatchDevice(StackDeviceMemory& res, int pb, bool useChecksum, uint32_
       // coalesce 28.4 -> 16 us at 8, 15.0 at 4, 19.2 at 16, same box)
       const uint32_t bpw = 4;
       dim3 g(std::max(1u, divUp(MB, bpw)), ny, kSegs);
+      CoalPrefix cp;
+      cp.flags = static_cast<const uint64_t*>(lease.base[kSyncFlags]);
+      cp.nW = nW;
+      cp.encBlocks = EncCfg<FT>::kBlocksPerWG;
+      cp.epoch = lease.epoch;
+      cp.err = deviceErrorWord();
       k_coalesce<FT><<<g, kThreads, 0, s>>>(in, out, y0, nb, std::max(MB, 1u), bpw, slots.data(),
                                             cw.data(), pdf, pb, useChecksum, ck.data(),
-                                            outSize_dev, sparseN);
+                                            outSize_dev, sparseN, cp);
       HIP_LAUNCH_CHECK();
     }
   }

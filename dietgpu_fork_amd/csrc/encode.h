@@ -997,6 +997,7 @@ __global__ __launch_bounds__(enc::kThreads) void k_encode(BatchDesc in, BatchDes
   __shared__ uint32_t cwE[Cfg::kBlocksPerWG];
   __shared__ uint32_t flE[Cfg::kBlocksPerWG];
   __shared__ uint32_t preE[Cfg::kBlocksPerWG];
+  __shared__ uint32_t cwSeg[kFused ? 1 : S][Cfg::kBlocksPerWG];  // fp64: word counts per segment
   __shared__ __attribute__((aligned(16))) uint16_t pdfS[kPro ? S : 1][kNumSymbols];
   static_assert(sizeof(ringS) >= S * kThreads * 16, "prologue scratch in the rings");
 
@@ -1231,12 +1232,34 @@ __global__ __launch_bounds__(enc::kThreads) void k_encode(BatchDesc in, BatchDes
         } else {
           gp<uint8_t> slot = G(slots) + ((uint64_t(s) * numInBatch + b) * MB + blk[c]) * kSlotBytes;
           ((gp<uint32_t>)slot)[l] = p.x;
-          if (l == 0) G(cw)[(uint64_t(s) * numInBatch + b) * MB + blk[c]] = words;
+          if (l == 0) {
+            G(cw)[(uint64_t(s) * numInBatch + b) * MB + blk[c]] = words;
+            cwSeg[kFused ? 0 : s][blk[c] - first] = words;
+          }
         }
       }
     }
   }
   }  // blk0 < nBlocks
+  if constexpr (!kFused) {
+    // fp64: one decoupled look-back per segment over the element's
+    // workgroups (wave s: segment s, side by side), so that k_coalesce reads
+    // each block range's prefix from the look-back flags instead of summing
+    // every earlier block's word count (quadratic in the blocks: a 1e8-word
+    // fp64 element's coalesce took 129 us for 211 MB).  The flags end as
+    // inclusive prefixes, per (segment, element, workgroup).
+    if (tail.flags) {
+      __syncthreads();
+      const uint32_t nk = first < nBlocks ? min(uint32_t(Cfg::kBlocksPerWG), nBlocks - first) : 0u;
+      if (w < uint32_t(S) && nk > 0) {
+        const uint32_t r = lane < nk ? roundUp(cwSeg[w][lane], 8) : 0u;
+        const uint32_t agg = readfirst(__shfl(waveInclusiveScan(r), 63));
+        bool pz = false;
+        (void)lookBackPoison(G(tail.flags) + (uint64_t(w) * numInBatch + b) * tail.nW, wx, agg, tail.epoch,
+                             tail.spinCap, pz);
+      }
+    }
+  }
   if constexpr (kFused) {
     // every wave's slot stores are complete before other waves copy them
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1286,12 +1309,25 @@ __device__ __forceinline__ uint32_t sumRoundedWords(gp<const uint32_t> cw, uint3
   return blockSum<kThreads>(v, red);
 }
 
+// CoalPrefix: the encoder's per-(segment, element) look-back flags (fp64:
+// k_encode<4> leaves each workgroup's inclusive prefix of rounded words in
+// its flag), so a block range's prefix and the segment totals are a few
+// loads instead of sums over every earlier block.  Null: sum the word counts.
+struct CoalPrefix {
+  const uint64_t* flags = nullptr;
+  uint32_t nW = 0;          // encode workgroups per element
+  uint32_t encBlocks = 0;   // blocks per encode workgroup
+  uint32_t epoch = 0;
+  uint32_t* err = nullptr;  // device error word (an element whose look-back poisoned)
+};
+
 template <int FT>
 __global__ __launch_bounds__(kThreads) void k_coalesce(
     BatchDesc in, BatchDesc out, uint32_t batchOffset, uint32_t numInBatch, uint32_t MB,
     uint32_t blocksPerWG, const uint8_t* __restrict__ slots, const uint32_t* __restrict__ cw,
     const uint16_t* __restrict__ pdf, int pb, bool useChecksum,
-    const uint32_t* __restrict__ ck, uint32_t* __restrict__ outSize, const uint32_t* __restrict__ sparseN) {
+    const uint32_t* __restrict__ ck, uint32_t* __restrict__ outSize, const uint32_t* __restrict__ sparseN,
+    CoalPrefix cp) {
   constexpr int kSegs = FloatTraits<FT>::kSegs;
   __shared__ uint32_t red[kWaves];
   __shared__ uint32_t pre[kThreads];
@@ -1307,12 +1343,40 @@ __global__ __launch_bounds__(kThreads) void k_coalesce(
   gp<const uint32_t> cw0 = G(cw) + uint64_t(b) * MB;
   gp<const uint32_t> cwS = G(cw) + (uint64_t(seg) * numInBatch + b) * MB;
 
+  // segment totals (inclusive prefix of the last encode workgroup) and the
+  // prefix before this range, from the encoder's flags
+  const bool fromFlags = cp.flags != nullptr && nBlocks > 0;
+  uint32_t segTotal[2] = {0, 0};
+  uint32_t flagBefore = 0, base = first;
+  if (fromFlags) {
+    const uint32_t eLast = (nBlocks - 1) / cp.encBlocks;
+    bool bad = false;
+    auto flagOf = [&](uint32_t s, uint32_t e) -> uint32_t {
+      const uint64_t v = G(cp.flags)[(uint64_t(s) * numInBatch + b) * cp.nW + e];
+      const uint32_t hi = uint32_t(v >> 32);
+      bad = bad || (v & kFlagPoisonE) != 0 || (hi >> 30) != 2u || (hi & kEpochMask) != cp.epoch;
+      return uint32_t(v);
+    };
+#pragma unroll
+    for (int s = 0; s < kSegs; ++s) segTotal[s] = flagOf(uint32_t(s), eLast);
+    const uint32_t e = min(first, nBlocks) / cp.encBlocks;
+    base = e * cp.encBlocks;
+    if (e > 0) flagBefore = flagOf(seg, e - 1);
+    if (bad) {  // an encoder look-back gave up: the element is abandoned
+      if (blockIdx.x == 0 && seg == 0 && tid == 0) {
+        if (outSize) G(outSize)[b] = 0u;
+        __hip_atomic_fetch_add(G(cp.err), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      return;
+    }
+  }
+
   gp<uint8_t> o = startOf(out, b);
   uint32_t total0Words = 0;
   if constexpr (FT != 0) {
     o += 32 + floatRawBytes(FT, n);
     if (kSegs == 2 && (seg == 1 || blockIdx.x == 0)) {
-      total0Words = sumRoundedWords(cw0, nBlocks, red);
+      total0Words = fromFlags ? segTotal[0] : sumRoundedWords(cw0, nBlocks, red);
       if (seg == 1) o += roundUp64(ansOverhead(nBlocks) + 2ull * total0Words, 16);
     }
   }
@@ -1320,18 +1384,22 @@ __global__ __launch_bounds__(kThreads) void k_coalesce(
   gp<uint2> bwords = (gp<uint2>)(states + uint64_t(kStateBytesPerBlock) * nBlocks);
   gp<uint8_t> data = (gp<uint8_t>)(bwords + roundUp(nBlocks, 2));
 
-  const uint32_t sumBefore = sumRoundedWords(cwS, min(first, nBlocks), red);
+  // exclusive scan over [base, last): base is this range's first block, or
+  // (flags) the first block of its encode workgroup, whose prefix the flag
+  // holds
+  const uint32_t sumBefore = fromFlags ? flagBefore : sumRoundedWords(cwS, min(first, nBlocks), red);
   const uint32_t last = min(first + blocksPerWG, nBlocks);
-  const uint32_t j = first + tid;
-  const uint32_t cwj = (tid < blocksPerWG && j < last) ? cwS[j] : 0u;
+  const uint32_t j = base + tid;
+  const uint32_t cwj = j < last ? cwS[j] : 0u;
   const uint32_t ex = blockExclusiveScan<kThreads>(roundUp(cwj, 8), red, nullptr) + sumBefore;
-  pre[tid] = ex;
+  if (j >= first && j < first + kThreads) pre[j - first] = ex;
   __syncthreads();
 
   if (blockIdx.x == 0) {
-    const uint32_t totalWords = sumRoundedWords(cwS, nBlocks, red);
+    const uint32_t totalWords = fromFlags ? segTotal[seg] : sumRoundedWords(cwS, nBlocks, red);
     uint32_t total1Words = 0;
-    if (kSegs == 2 && seg == 0) total1Words = sumRoundedWords(cwS + uint64_t(numInBatch) * MB, nBlocks, red);
+    if (kSegs == 2 && seg == 0)
+      total1Words = fromFlags ? segTotal[1] : sumRoundedWords(cwS + uint64_t(numInBatch) * MB, nBlocks, red);
     const uint64_t ansBytes = ansOverhead(nBlocks) + 2ull * totalWords;
     if (tid == 0) {
       gp<uint32_t> hdr = (gp<uint32_t>)o;
@@ -1384,7 +1452,7 @@ __global__ __launch_bounds__(kThreads) void k_coalesce(
   // per block: states (32 lanes) and the blockWords entry
   const uint32_t lane = tid & 63;
   __shared__ uint32_t cwL[kThreads];
-  cwL[tid] = cwj;
+  if (j >= first && j < first + kThreads) cwL[j - first] = cwj;
   for (uint32_t k = first + (tid >> 6); k < last; k += kWaves) {
     gp<const uint8_t> slot = G(slots) + ((uint64_t(seg) * numInBatch + b) * MB + k) * kSlotBytes;
     if (lane < 32)
