@@ -410,6 +410,15 @@ void encodeBatchDevice(StackDeviceMemory& res, int pb, bool useChecksum, uint32_
   // rows, in this stream's sync arena
   const size_t regions[kSyncRegions] = {0, size_t(kSegs) * nb * nW * 8, 0, 0, size_t(nb) * kSegs * 4, 0};
   SyncLease lease(res, s, regions, false, pro ? proRowsBytes : 0);
+  // fp64 (two segments): k_encode's per-segment look-back leaves each
+  // workgroup's prefix in its flag for k_coalesce, whose per-workgroup sums
+  // over every earlier block are otherwise quadratic in the blocks (1e8
+  // words: coalesce 129 us).  Below kCoalFlagBlocks blocks per element the
+  // sums are cheaper than the look-back's hand-offs (16.7M words: compress
+  // +1.5 us with it).
+  constexpr uint32_t kCoalFlagBlocks = 8192;
+  uint64_t* const flagsFor = (kFused || MB > kCoalFlagBlocks) ? static_cast<uint64_t*>(lease.base[kSyncFlags])
+                                                                : nullptr;
   NormArgs na;
   na.in = in;
   na.hist = userHist ? hist_dev : (reduce2 ? groupHist.data() : chunkRows);
@@ -427,8 +436,17 @@ void encodeBatchDevice(StackDeviceMemory& res, int pb, bool useChecksum, uint32_
   if (FT != 0 && useChecksum) {
     zeroAsync(ck.data(), sizeof(uint32_t) * nb, s);
   }
-  for (uint32_t y0 = 0; y0 < nb; y0 += kMaxGridY) {
-    const uint32_t ny = std::min(kMaxGridY, nb - y0);
+  // launch groups: histogram -> (normalise) -> encode per group of elements
+  // (kMallSliceBytes > 0: groups of about that many input bytes, so that the
+  // encoder re-reads its input from the 256 MiB Infinity Cache; 0: one group
+  // up to the grid limit)
+  constexpr size_t kMallSliceBytes = 0;
+  uint32_t slice = kMaxGridY;
+  if (kMallSliceBytes && runHist && !pro)
+    slice = uint32_t(std::max<size_t>(1, std::min<size_t>(kMaxGridY, kMallSliceBytes / std::max<size_t>(
+                                                                            1, size_t(maxSize) * sizeof(typename FloatTraits<FT>::WordT)))));
+  for (uint32_t y0 = 0; y0 < nb; y0 += slice) {
+    const uint32_t ny = std::min(slice, nb - y0);
     if (runHist) {
       prof::Scope p("hist", s);
       dim3 g(chunks, ny);
@@ -471,8 +489,8 @@ void encodeBatchDevice(StackDeviceMemory& res, int pb, bool useChecksum, uint32_
     if (MB > 0 || kFused) {
       prof::Scope p("encode", s);
       dim3 g(nW, ny);
-      EncTail tail{pdf, ck.data(), outSize_dev, static_cast<uint64_t*>(lease.base[kSyncFlags]), nW, pb,
-                   useChecksum, spinCap(), deviceErrorWord(), sparseN};
+      EncTail tail{pdf, ck.data(), outSize_dev, flagsFor, nW, pb, useChecksum, spinCap(), deviceErrorWord(),
+                   sparseN};
       tail.epoch = lease.epoch;
       tail.skew = dispatchSkew();
       if (pro) {
@@ -495,7 +513,7 @@ void encodeBatchDevice(StackDeviceMemory& res, int pb, bool useChecksum, uint32_
       const uint32_t bpw = 4;
       dim3 g(std::max(1u, divUp(MB, bpw)), ny, kSegs);
       CoalPrefix cp;
-      cp.flags = static_cast<const uint64_t*>(lease.base[kSyncFlags]);
+      cp.flags = flagsFor;
       cp.nW = nW;
       cp.encBlocks = EncCfg<FT>::kBlocksPerWG;
       cp.epoch = lease.epoch;

@@ -10,9 +10,11 @@
 // ONCE (k_sparseCount: bitmap, tile counts, nonzeros compacted within the
 // tile into a staging area; k_sparseGather: each tile sums its element's
 // earlier tile counts and moves its staged nonzeros to their list
-// positions), decompression takes the bitmap's tile popcounts
-// (k_sparseHeaders) and expands (k_sparseExpand, the same per-tile prefix).  (A decoupled look-back across the tiles of
-// one element measured slower: with thousands of tiles its chain dominates.)
+// positions); decompression counts the bitmap per 1024-word chunk
+// (k_sparseChunks), scans the counts per element (k_sparseChunkScan) and
+// expands one chunk per wave (k_sparseExpand).  (A decoupled look-back across
+// the tiles of one element measured slower: with thousands of tiles its
+// chain dominates.)
 //
 // Wire format: 16 B header {u32 N, 12 B zero}, bitmap
 // ceil(N/8) bytes (bit 7 of byte k <-> element 8k) padded to 16, then a dense
@@ -35,10 +37,6 @@ namespace dietgpu {
 namespace {
 
 constexpr uint32_t kTileWords = 4096;   // 4 waves x 16 steps x 64 lanes
-// tiles per k_sparseExpand workgroup: two (bitmap and list gathers of both
-// in the same two round trips) measured slower -- 1 x 15M fp32 decompress 59
-// -> 68 us: the doubled registers and LDS halved the resident workgroups
-constexpr uint32_t kExpandTiles = 1;
 constexpr uint32_t kMaxGridY = 65535;
 
 template <int FT>
@@ -285,126 +283,148 @@ __global__ __launch_bounds__(kThreads) void k_sparseGather(BatchDesc in, uint32_
   for (uint32_t i = threadIdx.x; i < cnt; i += kThreads) list[off + i] = st[i];
 }
 
-// d1: headers -> dense-archive pointers and sizes, and per-tile popcounts of
-// the bitmap.  grid (tiles, batch)
-__global__ __launch_bounds__(kThreads) void k_sparseHeaders(BatchDesc in, uint32_t batchOffset,
-                                                            uint32_t tilesPerElem,
-                                                            uint64_t* __restrict__ densePtrs,
-                                                            uint32_t* __restrict__ sizes,
-                                                            uint32_t* __restrict__ tileCounts) {
-  __shared__ uint32_t red[kWaves];
+// Decompression works on 1024-word chunks (16 bitmap words, one wave).
+constexpr uint32_t kChunkWords = 1024;
+
+// d1: one thread per chunk: the popcount of its 128 bitmap bytes (bits past
+// N masked: the bitmap's padding is the reference's uninitialised bytes), and
+// (chunk 0) the dense archive's address and N.  grid (ceil(chunks / 256),
+// batch).  A chunk's 128 B read may run past the padded bitmap into the
+// dense archive that follows it (>= 576 B), never past the archive.
+__global__ __launch_bounds__(kThreads) void k_sparseChunks(BatchDesc in, uint32_t batchOffset,
+                                                           uint32_t chunksPerElem,
+                                                           uint64_t* __restrict__ densePtrs,
+                                                           uint32_t* __restrict__ sizes,
+                                                           uint32_t* __restrict__ chunkPre) {
   const uint32_t b = batchOffset + blockIdx.y;
   gp<const uint8_t> a = (gp<const uint8_t>)in.start(b);
   const uint32_t n = ((gp<const uint32_t>)a)[0];
-  const uint32_t tile = blockIdx.x;
-  if (tile == 0 && threadIdx.x == 0) {
+  const uint32_t c = blockIdx.x * kThreads + threadIdx.x;
+  if (c == 0) {
     densePtrs[b] = reinterpret_cast<uint64_t>(in.start(b) + 16 + roundUp((n + 7) / 8, 16));
     sizes[b] = n;
   }
-  if (tile >= tilesPerElem) return;
-  // 512 bitmap bytes per tile: 2 bytes per thread
-  const uint32_t bytes0 = tile * (kTileWords / 8), bmBytes = (n + 7) / 8;
-  uint32_t c = 0;
-  for (uint32_t k = threadIdx.x; k < kTileWords / 8; k += kThreads)
-    if (bytes0 + k < bmBytes) c += __popc(a[16 + bytes0 + k]);
-  c = blockSum<kThreads>(c, red);
-  if (threadIdx.x == 0) tileCounts[uint64_t(b) * tilesPerElem + tile] = c;
+  if (c >= chunksPerElem) return;
+  uint32_t cnt = 0;
+  const uint32_t i0 = c * kChunkWords;
+  if (i0 < n) {
+    gp<const uint64_t> bm = (gp<const uint64_t>)(a + 16) + uint64_t(c) * (kChunkWords / 64);
+    uint64_t v[kChunkWords / 64];
+#pragma unroll
+    for (uint32_t k = 0; k < kChunkWords / 64; ++k) v[k] = i0 + 64 * k < n ? bm[k] : 0ull;
+#pragma unroll
+    for (uint32_t k = 0; k < kChunkWords / 64; ++k) {
+      const uint32_t e = i0 + 64 * k;
+      uint64_t m = v[k];
+      if (e < n && n - e < 64) m = maskToBitmap(m) & ((1ull << (n - e)) - 1);  // element order, tail cut
+      cnt += uint32_t(__popcll(m));
+    }
+  }
+  chunkPre[uint64_t(b) * chunksPerElem + c] = cnt;
+}
+
+// d2: in-place exclusive scan of each element's chunk counts, one workgroup
+// per element: thread t takes a contiguous run of the counts (16 B loads),
+// one block scan of the run sums, then the run's prefixes are written back.
+// grid (batch).
+__global__ __launch_bounds__(kThreads) void k_sparseChunkScan(uint32_t batchOffset, uint32_t chunksPerElem,
+                                                              const uint32_t* __restrict__ sizes,
+                                                              uint32_t* __restrict__ chunkPre) {
+  __shared__ uint32_t red[kWaves];
+  const uint32_t b = batchOffset + blockIdx.x;
+  const uint32_t chunks = min(chunksPerElem, divUp(sizes[b], kChunkWords));
+  gp<uint32_t> p = G(chunkPre) + uint64_t(b) * chunksPerElem;
+  const uint32_t run = roundUp(divUp(chunks, kThreads), 4);  // counts per thread, whole 16 B vectors
+  const uint32_t r0 = min(chunks, threadIdx.x * run), r1 = min(chunks, r0 + run);
+  // (chunksPerElem is a multiple of 4 and the rows 16 B aligned, see the host)
+  uint32_t sum = 0;
+#pragma unroll 4
+  for (uint32_t i = r0; i < r1; i += 4) {
+    const u32x4 q = *(gp<const u32x4>)(p + i);
+    sum += q.x + (i + 1 < r1 ? q.y : 0u) + (i + 2 < r1 ? q.z : 0u) + (i + 3 < r1 ? q.w : 0u);
+  }
+  uint32_t acc = blockExclusiveScan<kThreads>(sum, red, nullptr);
+#pragma unroll 4
+  for (uint32_t i = r0; i < r1; i += 4) {
+    const u32x4 q = *(gp<const u32x4>)(p + i);
+    u32x4 o;
+    o.x = acc;
+    acc += q.x;
+    o.y = acc;
+    acc += i + 1 < r1 ? q.y : 0u;
+    o.z = acc;
+    acc += i + 2 < r1 ? q.z : 0u;
+    o.w = acc;
+    acc += i + 3 < r1 ? q.w : 0u;
+    if (i + 4 <= r1) {
+      *(gp<u32x4>)(p + i) = o;
+    } else {
+      p[i] = o.x;
+      if (i + 1 < r1) p[i + 1] = o.y;
+      if (i + 2 < r1) p[i + 2] = o.z;
+    }
+  }
 }
 
 // d3: expand the decoded nonzero list into the output (fill_in_nonzeros
-// :95-144).  grid (ceil(tiles / kT), batch); a workgroup expands kT
-// consecutive 4096-word tiles: their bitmap words and the first tile's list
-// index (tilePrefix) in one memory round trip, the list gathers of all kT
-// tiles in a second, then 16 B streaming stores when the output is 16 B
-// aligned.  (kT = kExpandTiles: see there.)
-template <int FT, bool kVec, uint32_t kT>
+// :95-144).  One wave per 1024-word chunk (grid (ceil(chunks / 4), batch)),
+// no LDS and no barrier: lanes 0-15 load the chunk's 16 bitmap words
+// beside its list offset (the scanned chunk count), then for each 64-word
+// row the row's mask comes to SGPRs (readlane), each lane's list index is
+// offset + v_mbcnt of the mask, and all 16 rows' list gathers are issued
+// back to back (their addresses depend only on the bitmap) before the 16
+// row stores.  (The tile-per-workgroup kernel it replaces summed every
+// earlier tile's count per tile and staged through LDS: 5 x 15M fp32 at
+// 50 % zeros 176 us, fp64 430 us.)
+template <int FT>
 __global__ __launch_bounds__(kThreads) void k_sparseExpand(BatchDesc in, BatchDesc out, uint32_t batchOffset,
-                                                           uint32_t tilesPerElem, const uint32_t* __restrict__ sizes,
-                                                           const uint32_t* __restrict__ tileCounts,
-                                                           BatchDesc lists,
+                                                           uint32_t chunksPerElem, const uint32_t* __restrict__ sizes,
+                                                           const uint32_t* __restrict__ chunkPre, BatchDesc lists,
                                                            const uint8_t* __restrict__ denseOk,
                                                            uint8_t* __restrict__ outSuccess,
                                                            uint32_t* __restrict__ outSize) {
   using W = WordOf<FT>;
-  constexpr uint32_t kSteps = kTileWords / kWaves / 64;
-  constexpr uint32_t kVecs = kTileWords * sizeof(W) / 16 / kThreads;
-  __shared__ __attribute__((aligned(16))) W buf[kT][kTileWords];
-  __shared__ uint32_t waveCnt[kT][kWaves];
-  __shared__ uint32_t red[kWaves];
+  constexpr uint32_t kRows = kChunkWords / 64;
   const uint32_t b = batchOffset + blockIdx.y;
   const uint32_t n = sizes[b];
   const bool ok = denseOk[b] != 0 && out.size(b) >= n;
-  const uint32_t tile0 = blockIdx.x * kT;
-  const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  if (blockIdx.x == 0 && tid == 0) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
     if (outSuccess) outSuccess[b] = ok ? 1 : 0;
     if (outSize) outSize[b] = n;  // fill_in_nonzeros :107-109
   }
-  if (!ok || tile0 * kTileWords >= n) return;
+  const uint32_t lane = threadIdx.x & 63, w = readfirst(threadIdx.x >> 6);
+  const uint32_t c = blockIdx.x * kWaves + w;
+  const uint32_t i0 = c * kChunkWords;
+  if (!ok || c >= chunksPerElem || i0 >= n) return;
   gp<const uint8_t> bm = (gp<const uint8_t>)in.start(b) + 16;
-  uint64_t m[kT][kSteps];
-  uint32_t cnt[kT];
-#pragma unroll
-  for (uint32_t t = 0; t < kT; ++t) {
-    cnt[t] = 0;
-#pragma unroll
-    for (uint32_t j = 0; j < kSteps; ++j) {
-      const uint32_t i0 = (tile0 + t) * kTileWords + w * (kTileWords / kWaves) + 64 * j;
-      m[t][j] = i0 < n ? maskToBitmap(*(gp<const uint64_t>)(bm + i0 / 8)) : 0ull;
-      if (i0 < n && n - i0 < 64) m[t][j] &= (1ull << (n - i0)) - 1;
-      cnt[t] += uint32_t(__popcll(m[t][j]));
-    }
+  uint64_t mv = 0;
+  if (lane < kRows && i0 + 64 * lane < n) {
+    mv = maskToBitmap(*(gp<const uint64_t>)(bm + i0 / 8 + 8 * lane));
+    const uint32_t rem = n - (i0 + 64 * lane);
+    if (rem < 64) mv &= (1ull << rem) - 1;
   }
-  // the first tile's list index: the earlier tiles' popcounts (in flight
-  // together with the bitmap loads above)
-  uint32_t pos = tilePrefix(G(tileCounts) + uint64_t(b) * tilesPerElem, tile0, red);
-  if (lane == 0) {
-#pragma unroll
-    for (uint32_t t = 0; t < kT; ++t) waveCnt[t][w] = cnt[t];
-  }
-  __syncthreads();
+  uint32_t base = readfirst(G(chunkPre)[uint64_t(b) * chunksPerElem + c]);
+  // x[n-1] is read from idx[n-2] + 1 (fill_in_nonzeros :139-144): only the
+  // chunk holding word n-1 looks
+  const bool gap = n >= 2 && n - 1 - i0 < kChunkWords && ((bm[(n - 2) / 8] >> (7 - (n - 2) % 8)) & 1) == 0;
   gp<const W> list = (gp<const W>)lists.start(b);
-  // x[n-1] is read from idx[n-2] + 1 (fill_in_nonzeros :139-144)
-  const bool gap = n >= 2 && ((bm[(n - 2) / 8] >> (7 - (n - 2) % 8)) & 1) == 0;
+  W v[kRows];
 #pragma unroll
-  for (uint32_t t = 0; t < kT; ++t) {
-    uint32_t p = pos;
-    for (uint32_t k = 0; k < w; ++k) p += waveCnt[t][k];
-#pragma unroll
-    for (uint32_t j = 0; j < kSteps; ++j) {
-      const uint32_t q = w * (kTileWords / kWaves) + 64 * j + lane;
-      const uint32_t i = (tile0 + t) * kTileWords + q;
-      const bool f = (m[t][j] >> lane) & 1;
-      uint32_t src = p + mbcnt(m[t][j]);
-      if (i + 1 == n && gap) src += 1;
-      buf[t][q] = f ? list[src] : W(0);
-      p += uint32_t(__popcll(m[t][j]));
-    }
-    for (uint32_t k = 0; k < kWaves; ++k) pos += waveCnt[t][k];
+  for (uint32_t j = 0; j < kRows; ++j) {
+    const uint64_t m = (uint64_t(uint32_t(__builtin_amdgcn_readlane(int(uint32_t(mv >> 32)), int(j)))) << 32) |
+                       uint32_t(__builtin_amdgcn_readlane(int(uint32_t(mv)), int(j)));
+    const uint32_t i = i0 + 64 * j + lane;
+    uint32_t src = base + mbcnt(m);
+    if (gap && i + 1 == n) src += 1;
+    v[j] = (m >> lane) & 1 ? list[src] : W(0);
+    base += uint32_t(__popcll(m));
   }
-  __syncthreads();
   gp<W> y = (gp<W>)out.start(b);
 #pragma unroll
-  for (uint32_t t = 0; t < kT; ++t) {
-    const uint32_t t0 = (tile0 + t) * kTileWords;
-    if (t0 >= n) break;
-    const uint32_t tileN = min(kTileWords, n - t0);
-    if (kVec) {
-      constexpr uint32_t kWPV = 16 / sizeof(W);
-#pragma unroll
-      for (uint32_t v = 0; v < kVecs; ++v) {
-        const uint32_t wi = (v * kThreads + tid) * kWPV;
-        if (wi + kWPV <= tileN) {
-          const u32x4 val = *(lp<const u32x4>)&buf[t][wi];
-          // streaming: nothing here re-reads the output
-          st16nt((gp<uint4>)(y + t0 + wi), make_uint4(val.x, val.y, val.z, val.w));
-        } else {
-          for (uint32_t k = wi; k < tileN && k < wi + kWPV; ++k) y[t0 + k] = buf[t][k];
-        }
-      }
-    } else {
-      for (uint32_t i = tid; i < tileN; i += kThreads) y[t0 + i] = buf[t][i];
-    }
+  for (uint32_t j = 0; j < kRows; ++j) {
+    const uint32_t i = i0 + 64 * j + lane;
+    // streaming: nothing here re-reads the output
+    if (i < n) __builtin_nontemporal_store(v[j], y + i);
   }
 }
 
@@ -483,20 +503,23 @@ FloatDecompressStatus sparseDecompressT(StackDeviceMemory& res,
                                         const FloatDecompressConfig& config, uint32_t nb,
                                         const BatchDesc& in, const BatchDesc& out,
                                         uint32_t maxCap, uint8_t* outSuccess_dev,
-                                        uint32_t* outSize_dev, hipStream_t s, bool outAligned16) {
-  const uint32_t tiles = std::max(1u, divUp(maxCap, kTileWords));
+                                        uint32_t* outSize_dev, hipStream_t s) {
+  // chunk rows padded to 4 counts (16 B), for k_sparseChunkScan's vectors
+  const uint32_t chunks = roundUp(std::max(1u, divUp(maxCap, kChunkWords)), 4);
   auto densePtrs = res.alloc<uint64_t>(s, nb);
   auto sizes = res.alloc<uint32_t>(s, nb);
   auto denseOk = res.alloc<uint8_t>(s, nb);
   const uint64_t listStride = uint64_t(roundUp(maxCap, 16) + 16) * sizeof(WordOf<FT>);
   auto list = res.alloc<uint8_t>(s, size_t(nb) * listStride);
   const BatchDesc lists = BatchDesc::strided(list.data(), listStride, maxCap + 1);
-  auto tileCounts = res.alloc<uint32_t>(s, size_t(nb) * tiles);
+  auto chunkPre = res.alloc<uint32_t>(s, size_t(nb) * chunks);
   for (uint32_t y0 = 0; y0 < nb; y0 += kMaxGridY) {
     const uint32_t ny = std::min(kMaxGridY, nb - y0);
     prof::Scope p("sparse", s);
-    k_sparseHeaders<<<dim3(tiles, ny), kThreads, 0, s>>>(in, y0, tiles, densePtrs.data(), sizes.data(),
-                                                          tileCounts.data());
+    k_sparseChunks<<<dim3(divUp(chunks, kThreads), ny), kThreads, 0, s>>>(in, y0, chunks, densePtrs.data(),
+                                                                          sizes.data(), chunkPre.data());
+    HIP_LAUNCH_CHECK();
+    k_sparseChunkScan<<<ny, kThreads, 0, s>>>(y0, chunks, sizes.data(), chunkPre.data());
     HIP_LAUNCH_CHECK();
   }
   // dense decode of the nonzero list (capacity: the largest output)
@@ -525,16 +548,8 @@ FloatDecompressStatus sparseDecompressT(StackDeviceMemory& res,
   for (uint32_t y0 = 0; y0 < nb; y0 += kMaxGridY) {
     const uint32_t ny = std::min(kMaxGridY, nb - y0);
     prof::Scope p("sparse", s);
-    // (fp64: 32 KB per tile of LDS; one tile per workgroup)
-    constexpr uint32_t kT = sizeof(WordOf<FT>) <= 4 ? kExpandTiles : 1;
-    const dim3 g(divUp(tiles, kT), ny);
-    if (outAligned16) {
-      k_sparseExpand<FT, true, kT><<<g, kThreads, 0, s>>>(in, out, y0, tiles, sizes.data(), tileCounts.data(), lists,
-                                                           denseOk.data(), outSuccess_dev, outSize_dev);
-    } else {
-      k_sparseExpand<FT, false, kT><<<g, kThreads, 0, s>>>(in, out, y0, tiles, sizes.data(), tileCounts.data(), lists,
-                                                            denseOk.data(), outSuccess_dev, outSize_dev);
-    }
+    k_sparseExpand<FT><<<dim3(divUp(chunks, kWaves), ny), kThreads, 0, s>>>(
+        in, out, y0, chunks, sizes.data(), chunkPre.data(), lists, denseOk.data(), outSuccess_dev, outSize_dev);
     HIP_LAUNCH_CHECK();
   }
   return status;
@@ -625,8 +640,6 @@ FloatDecompressStatus floatDecompressSparse(StackDeviceMemory& res,
     cap[i] = outCapacity[i];
     maxCap = std::max(maxCap, cap[i]);
   }
-  bool aligned = true;
-  for (uint32_t i = 0; i < numInBatch; ++i) aligned = aligned && ptrs[numInBatch + i] % 16 == 0;
   GpuMemoryReservation<uint8_t> tbl;
   BatchDesc inD, outD;
   if (numInBatch == 1) {  // stride descriptors, no table upload
@@ -645,10 +658,10 @@ FloatDecompressStatus floatDecompressSparse(StackDeviceMemory& res,
     outD = BatchDesc::pointers(opD, capD);
   }
   switch (ft) {
-    case 1: return sparseDecompressT<1>(res, config, numInBatch, inD, outD, maxCap, outSuccess_dev, outSize_dev, stream, aligned);
-    case 2: return sparseDecompressT<2>(res, config, numInBatch, inD, outD, maxCap, outSuccess_dev, outSize_dev, stream, aligned);
-    case 3: return sparseDecompressT<3>(res, config, numInBatch, inD, outD, maxCap, outSuccess_dev, outSize_dev, stream, aligned);
-    default: return sparseDecompressT<4>(res, config, numInBatch, inD, outD, maxCap, outSuccess_dev, outSize_dev, stream, aligned);
+    case 1: return sparseDecompressT<1>(res, config, numInBatch, inD, outD, maxCap, outSuccess_dev, outSize_dev, stream);
+    case 2: return sparseDecompressT<2>(res, config, numInBatch, inD, outD, maxCap, outSuccess_dev, outSize_dev, stream);
+    case 3: return sparseDecompressT<3>(res, config, numInBatch, inD, outD, maxCap, outSuccess_dev, outSize_dev, stream);
+    default: return sparseDecompressT<4>(res, config, numInBatch, inD, outD, maxCap, outSuccess_dev, outSize_dev, stream);
   }
 }
 

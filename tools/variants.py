@@ -479,6 +479,12 @@ VARS["stampsm"] = SSTAMP
 # hand-off windows fall in the other slots' segment phases
 def STHALF(ticks):
     return [(P, "  if (iL >= A().items) return;\n", "  if (iL >= A().items) return;\n  if (blockIdx.x / A().slotSpan >= 2) {\n    const unsigned long long t0_ = __builtin_amdgcn_s_memrealtime();\n    while (__builtin_amdgcn_s_memrealtime() - t0_ < %dull) __builtin_amdgcn_s_sleep(8);\n  }\n" % ticks)]
+# round 6: the three-kernel path in launch groups whose input fits the MALL
+def MALLSL(mib):
+    return [("codec.hip", "  constexpr size_t kMallSliceBytes = 0;", "  constexpr size_t kMallSliceBytes = %dull << 20;" % mib)]
+VARS["sl128"] = MALLSL(128)
+VARS["sl192"] = MALLSL(192)
+VARS["sl384"] = MALLSL(384)
 VARS["sth5"] = STHALF(500)
 VARS["sth10"] = STHALF(1000)
 VARS["sth15"] = STHALF(1500)
