@@ -438,9 +438,54 @@ __global__ __launch_bounds__(dec::kThreads) __attribute__((amdgpu_num_sgpr(80)))
     if (blk0 >= nBlocks) break;
 
     // per pair c: blocks blk0 + 2c (lanes 0-31) and blk0 + 2c + 1 (lanes 32-63)
-    uint32_t uwH[K][2];  // wave-uniform
+    uint32_t uwH[K][2];  // wave-uniform: block sizes follow from n alone
     DStream st[K][S];
     lp<uint16_t> segLane[K][S];
+#pragma unroll
+    for (int c = 0; c < K; ++c)
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        const uint32_t bk = blk0 + 2 * c + hh;
+        uwH[c][hh] = bk < nBlocks ? min(kBlockSize, n - bk * kBlockSize) : 0u;
+      }
+    uint32_t T = 0;
+#pragma unroll
+    for (int c = 0; c < K; ++c) T = max(T, max(divUp(uwH[c][0], 32), divUp(uwH[c][1], 32)));
+    // segments [0, nFull) are full for every block of the wave; the partial
+    // top segments (element tail / odd block count) are decoded first, masked
+    uint32_t nFull = ~0u;
+#pragma unroll
+    for (int c = 0; c < K; ++c) nFull = min(nFull, min(uwH[c][0], uwH[c][1]) / dec::kSegWords);
+    const int32_t nSeg = int32_t(divUp(T, dec::kSegSteps));
+    const uint32_t off = dec::kChunk * l;  // this lane's chunk in a segment
+
+    // The pass's loads that do not depend on its blockWords go out first, in
+    // one memory round trip with them: the initial states and the raw float
+    // bytes of the first segment decoded (16 B-aligned full segments; the
+    // blockWords -> ring fill chain then starts behind them instead of ahead
+    // of them).  Cold archives: three dependent HBM round trips per pass
+    // became two.
+    uint32_t rvA[K][R], rvB[K][R];
+    const bool vecIO = vecIn && vecOut;
+    const bool rawEarly = FT != 0 && vecIO && nSeg > 0 && uint32_t(nSeg - 1) < nFull;
+    if (rawEarly) {
+#pragma unroll
+      for (int c = 0; c < K; ++c) {
+        const uint32_t bk = blk0 + 2 * c + (lane >> 5);
+        Join<FT>::load(rvA[c], raw, n, bk * kBlockSize + uint32_t(nSeg - 1) * dec::kSegWords + off);
+      }
+    }
+    uint32_t x0[K][S];
+#pragma unroll
+    for (int c = 0; c < K; ++c) {
+      const uint32_t bkMine = blk0 + 2 * c + (lane >> 5);
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        gp<const uint8_t> states = arch[s] + kANSHeaderBytes + kPdfBytes;
+        x0[c][s] = bkMine < nBlocks ? ((gp<const uint32_t>)(states + uint64_t(kStateBytesPerBlock) * bkMine))[l]
+                                    : kMinState;
+      }
+    }
 #pragma unroll
     for (int c = 0; c < K; ++c) {
 #pragma unroll
@@ -456,7 +501,6 @@ __global__ __launch_bounds__(dec::kThreads) __attribute__((amdgpu_num_sgpr(80)))
 #pragma unroll
         for (int hh = 0; hh < 2; ++hh) {
           const uint32_t bk = blk0 + 2 * c + hh;
-          uwH[c][hh] = 0;
           d.ptr[hh] = 0;
           d.lo[hh] = 0;
           d.data[hh] = data;
@@ -464,7 +508,6 @@ __global__ __launch_bounds__(dec::kThreads) __attribute__((amdgpu_num_sgpr(80)))
           if (bk < nBlocks) {
             const uint2 e = ld8(bw + bk);
             const uint32_t ex = readfirst(e.x), ey = readfirst(e.y);  // wave-uniform: SGPRs
-            uwH[c][hh] = ex >> 16;
             const int32_t cw = int32_t(ex & 0xffffu);
             d.ptr[hh] = cw;
             d.data[hh] = data + ey;
@@ -483,24 +526,9 @@ __global__ __launch_bounds__(dec::kThreads) __attribute__((amdgpu_num_sgpr(80)))
             ringPrefetch(d, hh, lane, vecIn);
           }
         }
-        const uint32_t bkMine = blk0 + 2 * c + (lane >> 5);
-        d.x = bkMine < nBlocks
-                  ? ((gp<const uint32_t>)(states + uint64_t(kStateBytesPerBlock) * bkMine))[l]
-                  : kMinState;
+        d.x = x0[c][s];
       }
     }
-
-    uint32_t T = 0;
-#pragma unroll
-    for (int c = 0; c < K; ++c) T = max(T, max(divUp(uwH[c][0], 32), divUp(uwH[c][1], 32)));
-
-    // segments [0, nFull) are full for every block of the wave; the partial
-    // top segments (element tail / odd block count) are decoded first, masked
-    uint32_t nFull = ~0u;
-#pragma unroll
-    for (int c = 0; c < K; ++c) nFull = min(nFull, min(uwH[c][0], uwH[c][1]) / dec::kSegWords);
-    const int32_t nSeg = int32_t(divUp(T, dec::kSegSteps));
-    const uint32_t off = dec::kChunk * l;  // this lane's chunk in a segment
 
     DStream* chains[K * S];
     lp<const u32x2> lutC[K * S];
@@ -520,7 +548,6 @@ __global__ __launch_bounds__(dec::kThreads) __attribute__((amdgpu_num_sgpr(80)))
       constexpr bool kVec = decltype(vecTag)::value;
       // raw float bytes, double-buffered: a full segment's bytes are loaded
       // before the previous segment's steps, a whole segment ahead of use
-      uint32_t rvA[K][R], rvB[K][R];
       auto loadRaw = [&](int32_t g, bool fullSeg, uint32_t (&rv)[K][R]) {
         const uint32_t segW0 = uint32_t(g) * dec::kSegWords;
 #pragma unroll
@@ -562,7 +589,7 @@ __global__ __launch_bounds__(dec::kThreads) __attribute__((amdgpu_num_sgpr(80)))
         }
       };
 
-      if (nSeg > 0) loadRaw(nSeg - 1, uint32_t(nSeg - 1) < nFull, rvA);
+      if (nSeg > 0 && !(kVec && rawEarly)) loadRaw(nSeg - 1, uint32_t(nSeg - 1) < nFull, rvA);
       // partial segments (a pair with an element's tail block, or with no
       // second block at all): masked steps, unrolled like the full segments
       // (constant LDS offsets, the ring checked every kUnroll steps); steps
