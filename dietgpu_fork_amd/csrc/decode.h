@@ -365,7 +365,7 @@ __device__ __forceinline__ void buildLut64(gp<const uint16_t> pdfIn, lp<u32x2> l
 // second generation.  (fp64, VGPR-bound at four workgroups per CU, spills a
 // few SGPRs to VGPR lanes instead: its decode time is unchanged.)
 template <int FT, int KK, bool NT, bool BAL>
-__global__ __launch_bounds__(dec::kThreads) __attribute__((amdgpu_num_sgpr(80))) void k_decode(const InlineTable,
+__global__ __launch_bounds__(dec::kThreads) __attribute__((amdgpu_num_sgpr(80), amdgpu_waves_per_eu(4))) void k_decode(const InlineTable,
                                                           BatchDesc in, BatchDesc out,
                                                           uint32_t batchOffset, int pb,
                                                           uint32_t chunksPerWG,
@@ -411,13 +411,6 @@ __global__ __launch_bounds__(dec::kThreads) __attribute__((amdgpu_num_sgpr(80)))
   const uint32_t nBlocks = divUp(n, kBlockSize);
   if (!success || blockIdx.x * chunksPerWG * Cfg::kBlocksPerWG >= nBlocks) return;
 
-#pragma unroll
-  for (int s = 0; s < S; ++s) {
-    buildLut64((gp<const uint16_t>)(arch[s] + kANSHeaderBytes),
-               (lp<u32x2>)(L + s * (lutBytes / S)), pb, (uint32_t*)segAll);
-    __syncthreads();
-  }
-
   const uint32_t w = readfirst(tid >> 6), lane = tid & 63, l = lane & 31;
   uint32_t hv = lane >= 32 ? ~0u : 0u;
   asm volatile("" : "+v"(hv));  // keep `hv & x` a v_and (not a v_cndmask pair)
@@ -431,11 +424,59 @@ __global__ __launch_bounds__(dec::kThreads) __attribute__((amdgpu_num_sgpr(80)))
 #pragma unroll
   for (int s = 0; s < S; ++s) lut[s] = (lp<const u32x2>)(L + s * (lutBytes / S));
 
+  // A pass's loads that do not depend on its blockWords -- the initial states
+  // and the raw float bytes of the first segment decoded (16 B-aligned full
+  // segments; block sizes follow from n) -- go out together with the
+  // blockWords, so that the blockWords -> ring fill chain no longer precedes
+  // them (cold archives: three dependent HBM round trips per pass became
+  // two).  The first pass's are issued before the decode-table build, whose
+  // pdf load and LDS passes they then overlap.
+  const bool vecIO = vecIn && vecOut;
+  uint32_t x0[K][S];
+  uint2 bwE[K][S][2];
+  uint32_t rvA[K][R], rvB[K][R];
+  auto issue = [&](uint32_t blk0) __attribute__((always_inline)) {
+    const uint32_t off = dec::kChunk * l;
+#pragma unroll
+    for (int c = 0; c < K; ++c) {
+      const uint32_t bkMine = blk0 + 2 * c + (lane >> 5);
+      // the first segment decoded is the block pair's top one; full (and so
+      // loadable unmasked) when both blocks of every pair are whole
+      const uint32_t uwMin = min(blk0 + 2 * c + 1 < nBlocks ? min(kBlockSize, n - (blk0 + 2 * c + 1) * kBlockSize) : 0u,
+                                 blk0 + 2 * c < nBlocks ? min(kBlockSize, n - (blk0 + 2 * c) * kBlockSize) : 0u);
+      if (FT != 0 && vecIO && uwMin == kBlockSize)
+        Join<FT>::load(rvA[c], raw, n, bkMine * kBlockSize + (kBlockSize / 32 / dec::kSegSteps - 1) * dec::kSegWords + off);
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        gp<const uint8_t> states = arch[s] + kANSHeaderBytes + kPdfBytes;
+        gp<const uint2> bw = (gp<const uint2>)(states + uint64_t(kStateBytesPerBlock) * nBlocks);
+        x0[c][s] = bkMine < nBlocks ? ((gp<const uint32_t>)(states + uint64_t(kStateBytesPerBlock) * bkMine))[l]
+                                    : kMinState;
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+          const uint32_t bk = blk0 + 2 * c + hh;
+          bwE[c][s][hh] = bk < nBlocks ? ld8(bw + bk) : make_uint2(0, 0);
+        }
+      }
+    }
+  };
+  {
+    const uint32_t blk00 = blockIdx.x * chunksPerWG * Cfg::kBlocksPerWG + w * Cfg::kBlocksPerWave;
+    if (blk00 < nBlocks) issue(blk00);
+  }
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    buildLut64((gp<const uint16_t>)(arch[s] + kANSHeaderBytes),
+               (lp<u32x2>)(L + s * (lutBytes / S)), pb, (uint32_t*)segAll);
+    __syncthreads();
+  }
+
   // Persistent over chunksPerWG consecutive chunks of this element (the grid
   // is one generation of resident workgroups; one table build per WG).
   for (uint32_t pass = 0; pass < chunksPerWG; ++pass) {
     const uint32_t blk0 = (blockIdx.x * chunksPerWG + pass) * Cfg::kBlocksPerWG + w * Cfg::kBlocksPerWave;
     if (blk0 >= nBlocks) break;
+    if (pass > 0) issue(blk0);
 
     // per pair c: blocks blk0 + 2c (lanes 0-31) and blk0 + 2c + 1 (lanes 32-63)
     uint32_t uwH[K][2];  // wave-uniform: block sizes follow from n alone
@@ -459,33 +500,7 @@ __global__ __launch_bounds__(dec::kThreads) __attribute__((amdgpu_num_sgpr(80)))
     const int32_t nSeg = int32_t(divUp(T, dec::kSegSteps));
     const uint32_t off = dec::kChunk * l;  // this lane's chunk in a segment
 
-    // The pass's loads that do not depend on its blockWords go out first, in
-    // one memory round trip with them: the initial states and the raw float
-    // bytes of the first segment decoded (16 B-aligned full segments; the
-    // blockWords -> ring fill chain then starts behind them instead of ahead
-    // of them).  Cold archives: three dependent HBM round trips per pass
-    // became two.
-    uint32_t rvA[K][R], rvB[K][R];
-    const bool vecIO = vecIn && vecOut;
     const bool rawEarly = FT != 0 && vecIO && nSeg > 0 && uint32_t(nSeg - 1) < nFull;
-    if (rawEarly) {
-#pragma unroll
-      for (int c = 0; c < K; ++c) {
-        const uint32_t bk = blk0 + 2 * c + (lane >> 5);
-        Join<FT>::load(rvA[c], raw, n, bk * kBlockSize + uint32_t(nSeg - 1) * dec::kSegWords + off);
-      }
-    }
-    uint32_t x0[K][S];
-#pragma unroll
-    for (int c = 0; c < K; ++c) {
-      const uint32_t bkMine = blk0 + 2 * c + (lane >> 5);
-#pragma unroll
-      for (int s = 0; s < S; ++s) {
-        gp<const uint8_t> states = arch[s] + kANSHeaderBytes + kPdfBytes;
-        x0[c][s] = bkMine < nBlocks ? ((gp<const uint32_t>)(states + uint64_t(kStateBytesPerBlock) * bkMine))[l]
-                                    : kMinState;
-      }
-    }
 #pragma unroll
     for (int c = 0; c < K; ++c) {
 #pragma unroll
@@ -506,7 +521,7 @@ __global__ __launch_bounds__(dec::kThreads) __attribute__((amdgpu_num_sgpr(80)))
           d.data[hh] = data;
           d.pf[hh] = u32x2{0, 0};
           if (bk < nBlocks) {
-            const uint2 e = ld8(bw + bk);
+            const uint2 e = bwE[c][s][hh];
             const uint32_t ex = readfirst(e.x), ey = readfirst(e.y);  // wave-uniform: SGPRs
             const int32_t cw = int32_t(ex & 0xffffu);
             d.ptr[hh] = cw;
