@@ -324,45 +324,44 @@ __global__ __launch_bounds__(kThreads) void k_sparseChunks(BatchDesc in, uint32_
 }
 
 // d2: in-place exclusive scan of each element's chunk counts, one workgroup
-// per element: thread t takes a contiguous run of the counts (16 B loads),
-// one block scan of the run sums, then the run's prefixes are written back.
-// grid (batch).
+// per element: thread t takes a contiguous run of the counts, at most
+// kScanVecs 16 B vectors of them at a time, all loaded in one round trip and
+// kept in registers; one block scan of the run sums, then the run's prefixes
+// are written back (a 15 M-word element's 14.6 K counts: one pass).  grid
+// (batch).
+constexpr uint32_t kScanVecs = 16;
 __global__ __launch_bounds__(kThreads) void k_sparseChunkScan(uint32_t batchOffset, uint32_t chunksPerElem,
                                                               const uint32_t* __restrict__ sizes,
                                                               uint32_t* __restrict__ chunkPre) {
   __shared__ uint32_t red[kWaves];
   const uint32_t b = batchOffset + blockIdx.x;
   const uint32_t chunks = min(chunksPerElem, divUp(sizes[b], kChunkWords));
-  gp<uint32_t> p = G(chunkPre) + uint64_t(b) * chunksPerElem;
-  const uint32_t run = roundUp(divUp(chunks, kThreads), 4);  // counts per thread, whole 16 B vectors
-  const uint32_t r0 = min(chunks, threadIdx.x * run), r1 = min(chunks, r0 + run);
   // (chunksPerElem is a multiple of 4 and the rows 16 B aligned, see the host)
-  uint32_t sum = 0;
-#pragma unroll 4
-  for (uint32_t i = r0; i < r1; i += 4) {
-    const u32x4 q = *(gp<const u32x4>)(p + i);
-    sum += q.x + (i + 1 < r1 ? q.y : 0u) + (i + 2 < r1 ? q.z : 0u) + (i + 3 < r1 ? q.w : 0u);
-  }
-  uint32_t acc = blockExclusiveScan<kThreads>(sum, red, nullptr);
-#pragma unroll 4
-  for (uint32_t i = r0; i < r1; i += 4) {
-    const u32x4 q = *(gp<const u32x4>)(p + i);
-    u32x4 o;
-    o.x = acc;
-    acc += q.x;
-    o.y = acc;
-    acc += i + 1 < r1 ? q.y : 0u;
-    o.z = acc;
-    acc += i + 2 < r1 ? q.z : 0u;
-    o.w = acc;
-    acc += i + 3 < r1 ? q.w : 0u;
-    if (i + 4 <= r1) {
-      *(gp<u32x4>)(p + i) = o;
-    } else {
-      p[i] = o.x;
-      if (i + 1 < r1) p[i + 1] = o.y;
-      if (i + 2 < r1) p[i + 2] = o.z;
+  gp<u32x4> p = (gp<u32x4>)(G(chunkPre) + uint64_t(b) * chunksPerElem);
+  const uint32_t nv = divUp(chunks, 4u);  // vectors (the last may be partial: its tail counts are 0)
+  uint32_t carry = 0;
+  for (uint32_t v0 = 0; v0 < nv; v0 += kScanVecs * kThreads) {
+    // this pass: vectors [v0, v0 + kScanVecs * kThreads), thread t a run of kScanVecs
+    const uint32_t r0 = v0 + threadIdx.x * kScanVecs;
+    u32x4 q[kScanVecs];
+    uint32_t sum = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kScanVecs; ++k) q[k] = r0 + k < nv ? p[r0 + k] : u32x4{0, 0, 0, 0};
+#pragma unroll
+    for (uint32_t k = 0; k < kScanVecs; ++k) sum += q[k].x + q[k].y + q[k].z + q[k].w;
+    uint32_t total = 0;
+    uint32_t acc = carry + blockExclusiveScan<kThreads>(sum, red, &total);
+#pragma unroll
+    for (uint32_t k = 0; k < kScanVecs; ++k) {
+      u32x4 o;
+      o.x = acc;
+      o.y = o.x + q[k].x;
+      o.z = o.y + q[k].y;
+      o.w = o.z + q[k].z;
+      acc = o.w + q[k].w;
+      if (r0 + k < nv) p[r0 + k] = o;
     }
+    carry += total;
   }
 }
 
