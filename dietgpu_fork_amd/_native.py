@@ -115,7 +115,8 @@ def testlib():
         c_u32, c_int, P = ctypes.c_uint32, ctypes.c_int, ctypes.c_void_p
         sig = {"dietgpu_test_last_error": (ctypes.c_char_p, []),
                "dietgpu_test_occupy": (c_int, [P, c_u32, c_u32, c_u32]),
-               "dietgpu_test_histogram": (c_int, [P, c_u32, P, c_u32, c_u32, P, P])}
+               "dietgpu_test_histogram": (c_int, [P, c_u32, P, c_u32, c_u32, P, P]),
+               "dietgpu_test_enc_magic": (c_int, [P, P])}
         for name, (res, args) in sig.items():
             f = getattr(T, name)
             f.restype = res

@@ -47,6 +47,14 @@ def test_histogram(x2d, size=None, ws=None):
     return hist
 
 
+def test_enc_magic(device="cuda"):
+    """Test hook (libdietgpu_testhooks.so): the compressors' in-register
+    division magic of every pdf 0 .. 2048, as an int64 CPU tensor."""
+    m = torch.empty([(1 << 11) + 1], dtype=torch.int32, device=device)
+    N.test_check(N.testlib().dietgpu_test_enc_magic(m.data_ptr(), _s()))
+    return m.cpu().to(torch.int64) & 0xffffffff
+
+
 def max_compressed_size(nbytes):
     return N.size_or_raise(N.lib().dietgpu_get_max_compressed_size(int(nbytes)))
 

@@ -16,6 +16,7 @@
 #include <mutex>
 #include <sstream>
 #include <tuple>
+#include <type_traits>
 #include <vector>
 
 #include "codec_internal.h"
@@ -140,18 +141,42 @@ DeviceTables uploadTables(StackDeviceMemory& res, hipStream_t s, uint32_t nb,
 
 // Device copy of inline tables for kernels without an InlineTable argument,
 // allocated in the calling driver's scope (the arena is LIFO) and only when
-// the tables are inline.
+// the tables are inline.  A one-element batch needs no copy at all: its
+// descriptors become stride descriptors of that element (its address, and
+// its size as the fixed size), so the three-kernel path of a batch-1
+// pointer / split-size call launches no upload kernel (fp64 1 x 16M words
+// and the float_benchmark's batch-1 grid: a 4.7 us k_table launch before
+// k_hist).
 struct DeviceDescs {
   GpuMemoryReservation<uint8_t> mem;
   uintptr_t base = 0;
-  DeviceDescs(StackDeviceMemory& res, hipStream_t s, const DeviceTables* t) {
+  const InlineTable* single = nullptr;  // nb == 1: entries read from the kernarg image
+  DeviceDescs(StackDeviceMemory& res, hipStream_t s, const DeviceTables* t, uint32_t nb) {
     if (!t || !t->inl) return;
+    if (nb == 1) {
+      single = t->image.get();
+      return;
+    }
     mem = res.alloc<uint8_t>(s, std::max<size_t>(t->host.size(), 1));
     StackDeviceMemory::copyToDevice(mem.data(), t->host.data(), t->host.size(), s);
     base = reinterpret_cast<uintptr_t>(mem.data()) - kInlineBias;
   }
   BatchDesc map(BatchDesc d) const {
     if (!d.inl) return d;
+    if (single) {
+      auto entry = [&](auto p) {
+        using T = std::remove_cv_t<std::remove_pointer_t<decltype(p)>>;
+        T v;
+        std::memcpy(&v, reinterpret_cast<const uint8_t*>(single->w) + reinterpret_cast<uintptr_t>(p), sizeof(T));
+        return v;
+      };
+      uint8_t* start = d.mode == BatchDesc::kPointer ? reinterpret_cast<uint8_t*>(entry(d.ptrs))
+                       : d.mode == BatchDesc::kSplit ? d.base + entry(d.offsets)
+                                                     : d.base;
+      DG_CHECK(!d.sizes || (d.inl & BatchDesc::kInlSizes), "mixed inline / device size table");
+      const uint32_t size = d.sizes ? entry(d.sizes) : d.fixedSize;
+      return BatchDesc::strided(start, 0, size);
+    }
     auto rebase = [&](auto p) { return reinterpret_cast<decltype(p)>(base + reinterpret_cast<uintptr_t>(p)); };
     if (d.inl & BatchDesc::kInlPtrs) d.ptrs = rebase(d.ptrs);
     if (d.inl & BatchDesc::kInlSizes) d.sizes = rebase(d.sizes);
@@ -277,7 +302,7 @@ bool compressPersistent(StackDeviceMemory& res, int pb, bool useChecksum, uint32
 
   auto slotMem = res.alloc<uint8_t>(s, size_t(grid) * pc::kBlocksPerItem * kSlotDataBytes);
   auto ck = res.alloc<uint32_t>(s, FT != 0 && useChecksum ? nb : 1);
-  DeviceDescs dd(res, s, FT != 0 && useChecksum ? tabs : nullptr);  // k_checksum's view
+  DeviceDescs dd(res, s, FT != 0 && useChecksum ? tabs : nullptr, nb);  // k_checksum's view
   // epoch-tagged state in this stream's persistent arena (no per-call
   // zeroing), one region per kind of word: the dequeue counters (at a fixed
   // place: a call zeroes the next call's), the look-back flags, the tagged
@@ -364,7 +389,7 @@ void encodeBatchDevice(StackDeviceMemory& res, int pb, bool useChecksum, uint32_
     }
   }
   // three-kernel path: plain device tables
-  DeviceDescs dd(res, s, tabs);
+  DeviceDescs dd(res, s, tabs, nb);
   const BatchDesc in = dd.map(inArg), out = dd.map(outArg);
 
   // Prologue normalisation (k_encode<.., kPro>, encode.h proNormalize):
@@ -584,7 +609,7 @@ std::vector<std::pair<int, std::string>> verifyChecksums(StackDeviceMemory& res,
                                                          const DeviceTables* tabs) {
   std::vector<std::pair<int, std::string>> errs;
   if (nb == 0) return errs;
-  DeviceDescs dd(res, s, tabs);
+  DeviceDescs dd(res, s, tabs, nb);
   const BatchDesc archives = dd.map(archivesArg), decoded = dd.map(decodedArg);
   auto now = res.alloc<uint32_t>(s, nb);
   auto old = res.alloc<uint32_t>(s, nb);

@@ -152,19 +152,44 @@ __device__ __forceinline__ uint4 encTableEntry(uint32_t q, uint32_t cdf, int pb)
   return encEntryPack(q, cdf, magic, shift, pb);
 }
 
-// The same entry with the magic computed in registers (no dependent global
-// load of kMagic on a latency-bound path): ceil(2^(31+l) / q) from a double
-// division (the numerator 2^(31+l) <= 2^42 is exact; the quotient is within
-// one of the floor) and an exact integer fix-up.
+// The magic of pdf q >= 2 computed in registers (no dependent global load of
+// kMagic on a latency-bound path): ceil(2^(32+shift) / q) from v_rcp_f64 and
+// two Newton steps (any seed better than 2^-8 relative then lands within one
+// of the quotient: it is below 2^32), and an exact fix-up -- the remainder
+// 2^(32+shift) - m q is an integer below 2^13 in magnitude, so one fma yields
+// it exactly.  About a quarter of the IEEE double division it replaced
+// (v_div_scale / v_div_fmas / v_div_fixup and three 64-bit integer products
+// per entry), which sat on the compressor's hand-off window.  Exhaustively
+// checked against encMagic (dietgpu_test_enc_magic, tests/test_gpu_kat.py).
+__device__ __forceinline__ uint32_t encMagicReg(uint32_t q, uint32_t shift) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const double qd = double(q);
+  double r = __builtin_amdgcn_rcp(qd);
+  r = __builtin_fma(r, __builtin_fma(-qd, r, 1.0), r);
+  r = __builtin_fma(r, __builtin_fma(-qd, r, 1.0), r);
+  const int e = int(32 + shift);
+  double m = __builtin_floor(__builtin_amdgcn_ldexp(r, e));
+  double rem = __builtin_fma(-m, qd, __builtin_amdgcn_ldexp(1.0, e));
+  if (rem < 0.0) {
+    m -= 1.0;
+    rem += qd;
+  } else if (rem >= qd) {
+    m += 1.0;
+    rem -= qd;
+  }
+  return uint32_t(m) + (rem != 0.0 ? 1u : 0u);
+#else
+  uint32_t sh = 0;
+  (void)shift;
+  return encMagic(q, &sh);
+#endif
+}
+
 __device__ __forceinline__ uint4 encTableEntryReg(uint32_t q, uint32_t cdf, int pb) {
   uint32_t shift = 0, magic = 0;
   if (q > 1) {
     shift = 31 - __clz(q - 1);
-    const uint64_t num = 1ull << (32 + shift);
-    uint64_t m = uint64_t(double(num) / double(q));  // ~floor(num / q)
-    if (m * q > num) m -= 1;
-    else if ((m + 1) * q <= num) m += 1;
-    magic = uint32_t(m + (m * q != num));  // ceil
+    magic = encMagicReg(q, shift);
   } else if (q == 1) {
     magic = 0xffffffffu;
   }

@@ -10,9 +10,10 @@
 // ONCE (k_sparseCount: bitmap, tile counts, nonzeros compacted within the
 // tile into a staging area; k_sparseGather: each tile sums its element's
 // earlier tile counts and moves its staged nonzeros to their list
-// positions); decompression counts the bitmap per 1024-word chunk
-// (k_sparseChunks), scans the counts per element (k_sparseChunkScan) and
-// expands one chunk per wave (k_sparseExpand).  (A decoupled look-back across
+// positions); decompression counts the bitmap per 1024-word chunk and scans
+// the counts within each workgroup of 256 chunks (k_sparseChunks), then
+// expands one chunk per wave, adding the element's earlier workgroups' totals
+// (k_sparseExpand).  (A decoupled look-back across
 // the tiles of one element measured slower: with thousands of tiles its
 // chain dominates.)
 //
@@ -23,6 +24,7 @@
 // slot (written as 0 here, uninitialised in the reference) precedes x[N-1].
 #include <algorithm>
 #include <cstring>
+#include <optional>
 #include <vector>
 
 #include "codec_internal.h"
@@ -31,6 +33,7 @@
 #include "decode.h"
 #include "encode.h"
 #include "profile.h"
+#include "sync_arena.h"
 
 namespace dietgpu {
 
@@ -85,8 +88,8 @@ template <int FT, bool kVec, bool kHist, typename W, typename HS>
 __device__ __forceinline__ void sparseCountTile(const BatchDesc& in, gp<uint8_t> o, uint32_t b, uint32_t n,
                                                 uint32_t tile, uint32_t numInBatch, uint32_t tilesPerElem,
                                                 uint32_t* __restrict__ tileCounts, W* __restrict__ staging,
-                                                uint32_t* __restrict__ histRows, uint32_t nRows, W* buf, HS& hs,
-                                                uint32_t* waveCnt) {
+                                                uint32_t* __restrict__ histRows, uint32_t* __restrict__ zeroNext,
+                                                uint32_t nRows, W* buf, HS& hs, uint32_t* waveCnt) {
   constexpr int kSegs = FloatTraits<FT>::kSegs;
   constexpr uint32_t kSteps = kTileWords / kWaves / 64;
   constexpr uint32_t kCols = 4;  // LDS counter columns per bin (lane & 3)
@@ -164,9 +167,12 @@ __device__ __forceinline__ void sparseCountTile(const BatchDesc& in, gp<uint8_t>
 #pragma unroll
       for (uint32_t k = 0; k < kCols; ++k) sum += hs[sg][tid * kCols + ((k + tid) & (kCols - 1))];
       // few adds per address: the tiles of an element spread over nRows rows
+      const uint64_t row = (uint64_t(sg) * numInBatch + b) * nRows + tile % nRows;
       if (sum)
-        __hip_atomic_fetch_add(G(histRows) + ((uint64_t(sg) * numInBatch + b) * nRows + tile % nRows) * kNumSymbols + tid,
-                               sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(G(histRows) + row * kNumSymbols + tid, sum, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+      // the same row of the arena's other buffer, zeroed for the next call
+      if (tile < nRows) G(zeroNext)[row * kNumSymbols + tid] = 0;
     }
   }
 }
@@ -184,9 +190,12 @@ __device__ __forceinline__ void sparseCountTile(const BatchDesc& in, gp<uint8_t>
 //
 // kHist: the staged words are also counted into the dense codec's symbol
 // histogram(s) (the compacted list's symbols, the n-2 slot included) and
-// added into row tile % nRows of [segments][nb][nRows][256] (PartialHist,
-// zeroed by the host), so the dense codec skips its histogram pass over the
-// list.  (Normalising in the element's last-arriving tile instead of the
+// added into row tile % nRows of [segments][nb][nRows][256] (PartialHist),
+// so the dense codec skips its histogram pass over the list.  The rows are
+// the stream's sync-arena row buffer (SyncLease::rows, zero on entry); the
+// first nRows tiles zero the same rows of the other buffer for the next call
+// (`zeroNext`), so no zeroing launch precedes this one (1 x 15M fp32: a
+// 4.7 us k_zero of 64 KB before).  (Normalising in the element's last-arriving tile instead of the
 // dense codec's k_normalize launch made every tile pay a store drain and a
 // counter round trip: c4 1 x 15M fp32 compress 70 -> 95 us.)
 // (at most 80 SGPRs: 86-94 admit 7 workgroups per CU instead of 8,
@@ -197,7 +206,8 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_num_sgpr(80))) void
                                                           uint32_t tilesPerElem,
                                                           uint32_t* __restrict__ tileCounts,
                                                           WordOf<FT>* __restrict__ staging,
-                                                          uint32_t* __restrict__ histRows, uint32_t nRows) {
+                                                          uint32_t* __restrict__ histRows,
+                                                          uint32_t* __restrict__ zeroNext, uint32_t nRows) {
   using W = WordOf<FT>;
   constexpr int kSegs = FloatTraits<FT>::kSegs;
   constexpr uint32_t kCols = 4;  // LDS counter columns per bin (lane & 3)
@@ -215,7 +225,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_num_sgpr(80))) void
     if (tid == 0) tileCounts[uint64_t(b) * tilesPerElem + tile] = 0;
   } else {
     sparseCountTile<FT, kVec, kHist>(in, o, b, n, tile, numInBatch, tilesPerElem, tileCounts, staging, histRows,
-                                     nRows, buf, hs, waveCnt);
+                                     zeroNext, nRows, buf, hs, waveCnt);
   }
 }
 
@@ -287,15 +297,23 @@ __global__ __launch_bounds__(kThreads) void k_sparseGather(BatchDesc in, uint32_
 constexpr uint32_t kChunkWords = 1024;
 
 // d1: one thread per chunk: the popcount of its 128 bitmap bytes (bits past
-// N masked: the bitmap's padding is the reference's uninitialised bytes), and
-// (chunk 0) the dense archive's address and N.  grid (ceil(chunks / 256),
-// batch).  A chunk's 128 B read may run past the padded bitmap into the
-// dense archive that follows it (>= 576 B), never past the archive.
+// N masked: the bitmap's padding is the reference's uninitialised bytes),
+// then the workgroup's exclusive scan of its 256 chunk counts: chunkPre[c] =
+// the count of the earlier chunks of c's workgroup, blockTot[g] = workgroup
+// g's total; (chunk 0) the dense archive's address and N.  grid
+// (ceil(chunks / 256), batch).  The expansion adds the earlier workgroups'
+// totals itself (k_sparseExpand), so no scan launch or cross-workgroup
+// hand-off follows (a separate one-workgroup-per-element scan launch: 1 x 15M
+// fp32 decompress 5.8 us more).  A chunk's 128 B read may run past the padded
+// bitmap into the dense archive that follows it (>= 576 B), never past the
+// archive.
 __global__ __launch_bounds__(kThreads) void k_sparseChunks(BatchDesc in, uint32_t batchOffset,
-                                                           uint32_t chunksPerElem,
+                                                           uint32_t chunksPerElem, uint32_t blocksPerElem,
                                                            uint64_t* __restrict__ densePtrs,
                                                            uint32_t* __restrict__ sizes,
-                                                           uint32_t* __restrict__ chunkPre) {
+                                                           uint32_t* __restrict__ chunkPre,
+                                                           uint32_t* __restrict__ blockTot) {
+  __shared__ uint32_t red[kWaves];
   const uint32_t b = batchOffset + blockIdx.y;
   gp<const uint8_t> a = (gp<const uint8_t>)in.start(b);
   const uint32_t n = ((gp<const uint32_t>)a)[0];
@@ -304,10 +322,9 @@ __global__ __launch_bounds__(kThreads) void k_sparseChunks(BatchDesc in, uint32_
     densePtrs[b] = reinterpret_cast<uint64_t>(in.start(b) + 16 + roundUp((n + 7) / 8, 16));
     sizes[b] = n;
   }
-  if (c >= chunksPerElem) return;
   uint32_t cnt = 0;
   const uint32_t i0 = c * kChunkWords;
-  if (i0 < n) {
+  if (c < chunksPerElem && i0 < n) {
     gp<const uint64_t> bm = (gp<const uint64_t>)(a + 16) + uint64_t(c) * (kChunkWords / 64);
     uint64_t v[kChunkWords / 64];
 #pragma unroll
@@ -320,49 +337,10 @@ __global__ __launch_bounds__(kThreads) void k_sparseChunks(BatchDesc in, uint32_
       cnt += uint32_t(__popcll(m));
     }
   }
-  chunkPre[uint64_t(b) * chunksPerElem + c] = cnt;
-}
-
-// d2: in-place exclusive scan of each element's chunk counts, one workgroup
-// per element: thread t takes a contiguous run of the counts, at most
-// kScanVecs 16 B vectors of them at a time, all loaded in one round trip and
-// kept in registers; one block scan of the run sums, then the run's prefixes
-// are written back (a 15 M-word element's 14.6 K counts: one pass).  grid
-// (batch).
-constexpr uint32_t kScanVecs = 16;
-__global__ __launch_bounds__(kThreads) void k_sparseChunkScan(uint32_t batchOffset, uint32_t chunksPerElem,
-                                                              const uint32_t* __restrict__ sizes,
-                                                              uint32_t* __restrict__ chunkPre) {
-  __shared__ uint32_t red[kWaves];
-  const uint32_t b = batchOffset + blockIdx.x;
-  const uint32_t chunks = min(chunksPerElem, divUp(sizes[b], kChunkWords));
-  // (chunksPerElem is a multiple of 4 and the rows 16 B aligned, see the host)
-  gp<u32x4> p = (gp<u32x4>)(G(chunkPre) + uint64_t(b) * chunksPerElem);
-  const uint32_t nv = divUp(chunks, 4u);  // vectors (the last may be partial: its tail counts are 0)
-  uint32_t carry = 0;
-  for (uint32_t v0 = 0; v0 < nv; v0 += kScanVecs * kThreads) {
-    // this pass: vectors [v0, v0 + kScanVecs * kThreads), thread t a run of kScanVecs
-    const uint32_t r0 = v0 + threadIdx.x * kScanVecs;
-    u32x4 q[kScanVecs];
-    uint32_t sum = 0;
-#pragma unroll
-    for (uint32_t k = 0; k < kScanVecs; ++k) q[k] = r0 + k < nv ? p[r0 + k] : u32x4{0, 0, 0, 0};
-#pragma unroll
-    for (uint32_t k = 0; k < kScanVecs; ++k) sum += q[k].x + q[k].y + q[k].z + q[k].w;
-    uint32_t total = 0;
-    uint32_t acc = carry + blockExclusiveScan<kThreads>(sum, red, &total);
-#pragma unroll
-    for (uint32_t k = 0; k < kScanVecs; ++k) {
-      u32x4 o;
-      o.x = acc;
-      o.y = o.x + q[k].x;
-      o.z = o.y + q[k].y;
-      o.w = o.z + q[k].z;
-      acc = o.w + q[k].w;
-      if (r0 + k < nv) p[r0 + k] = o;
-    }
-    carry += total;
-  }
+  uint32_t total = 0;
+  const uint32_t excl = blockExclusiveScan<kThreads>(cnt, red, &total);
+  if (c < chunksPerElem) chunkPre[uint64_t(b) * chunksPerElem + c] = excl;
+  if (threadIdx.x == 0) blockTot[uint64_t(b) * blocksPerElem + blockIdx.x] = total;
 }
 
 // d3: expand the decoded nonzero list into the output (fill_in_nonzeros
@@ -377,8 +355,10 @@ __global__ __launch_bounds__(kThreads) void k_sparseChunkScan(uint32_t batchOffs
 // 50 % zeros 176 us, fp64 430 us.)
 template <int FT>
 __global__ __launch_bounds__(kThreads) void k_sparseExpand(BatchDesc in, BatchDesc out, uint32_t batchOffset,
-                                                           uint32_t chunksPerElem, const uint32_t* __restrict__ sizes,
-                                                           const uint32_t* __restrict__ chunkPre, BatchDesc lists,
+                                                           uint32_t chunksPerElem, uint32_t blocksPerElem,
+                                                           const uint32_t* __restrict__ sizes,
+                                                           const uint32_t* __restrict__ chunkPre,
+                                                           const uint32_t* __restrict__ blockTot, BatchDesc lists,
                                                            const uint8_t* __restrict__ denseOk,
                                                            uint8_t* __restrict__ outSuccess,
                                                            uint32_t* __restrict__ outSize) {
@@ -402,7 +382,15 @@ __global__ __launch_bounds__(kThreads) void k_sparseExpand(BatchDesc in, BatchDe
     const uint32_t rem = n - (i0 + 64 * lane);
     if (rem < 64) mv &= (1ull << rem) - 1;
   }
-  uint32_t base = readfirst(G(chunkPre)[uint64_t(b) * chunksPerElem + c]);
+  // the chunk's list offset: its count prefix within its k_sparseChunks
+  // workgroup plus the totals of the element's earlier workgroups, loaded
+  // in the bitmap's round trip (one load per lane up to 64 workgroups, i.e.
+  // 16 M words)
+  const uint32_t g = c / kThreads;
+  uint32_t part = 0;
+  for (uint32_t k0 = 0; k0 < g; k0 += 64)
+    part += k0 + lane < g ? G(blockTot)[uint64_t(b) * blocksPerElem + k0 + lane] : 0u;
+  uint32_t base = readfirst(G(chunkPre)[uint64_t(b) * chunksPerElem + c]) + waveSum(part);
   // x[n-1] is read from idx[n-2] + 1 (fill_in_nonzeros :139-144): only the
   // chunk holding word n-1 looks
   const bool gap = n >= 2 && n - 1 - i0 < kChunkWords && ((bm[(n - 2) / 8] >> (7 - (n - 2) % 8)) & 1) == 0;
@@ -456,16 +444,22 @@ void sparseCompressT(StackDeviceMemory& res, const FloatCompressConfig& config, 
   bool countHist = nb == 1;
   if constexpr (FT != 4) countHist = countHist && !persistentPreferred<FT>(nb, maxN);
   constexpr int kSegs = FloatTraits<FT>::kSegs;
-  // histogram rows: up to 64 per element, accumulated with atomics
+  // histogram rows: up to 64 per element, accumulated with atomics into this
+  // stream's sync-arena row buffer (zero on entry; k_sparseCount zeroes the
+  // other buffer for the next call).  The lease is released before the dense
+  // codec takes its own.
   const uint32_t G = tiles;
   const uint32_t R = std::min(tiles, kReduceRows);
-  auto hist = res.alloc<uint32_t>(s, countHist ? size_t(kSegs) * nb * R * kNumSymbols : 1);
-  if (countHist) zeroAsync(hist.data(), size_t(kSegs) * nb * R * kNumSymbols * 4, s);
+  const size_t rowsBytes = countHist ? size_t(kSegs) * nb * R * kNumSymbols * 4 : 0;
+  std::optional<SyncLease> lease;
+  if (countHist) lease.emplace(res, s, kNoSyncRegions, false, rowsBytes);
+  uint32_t* const histRows = countHist ? static_cast<uint32_t*>(lease->rows[0]) : nullptr;
+  uint32_t* const zeroNext = countHist ? static_cast<uint32_t*>(lease->rows[1]) : nullptr;
   auto table = res.alloc<uint4>(s, countHist ? size_t(kSegs) * nb * kNumSymbols : 1);
   auto pdf = res.alloc<uint16_t>(s, countHist ? size_t(kSegs) * nb * kNumSymbols : 1);
   NormArgs na{};
   na.in = in;
-  na.hist = hist.data();
+  na.hist = histRows;
   na.rows = R;
   na.pb = config.ansConfig.probBits;
   na.table = table.data();
@@ -476,7 +470,7 @@ void sparseCompressT(StackDeviceMemory& res, const FloatCompressConfig& config, 
     prof::Scope p("sparse", s);
     auto launch = [&](auto vecTag, auto histTag) {
       k_sparseCount<FT, decltype(vecTag)::value, decltype(histTag)::value><<<dim3(G, ny), kThreads, 0, s>>>(
-          in, outD, y0, nb, tiles, tileCounts.data(), staging.data(), hist.data(), R);
+          in, outD, y0, nb, tiles, tileCounts.data(), staging.data(), histRows, zeroNext, R);
     };
     if (inAligned16) {
       if (countHist) launch(std::true_type{}, std::true_type{});
@@ -490,7 +484,8 @@ void sparseCompressT(StackDeviceMemory& res, const FloatCompressConfig& config, 
         in, y0, nb, tiles, tileCounts.data(), listLen.data(), staging.data(), lists, na);
     HIP_LAUNCH_CHECK();
   }
-  PartialHist pre{hist.data(), R};
+  lease.reset();
+  PartialHist pre{histRows, R};
   pre.table = table.data();
   pre.pdf = pdf.data();
   floatCompressDescs(res, config, nb, lists, maxN, denseOut, outSize_dev, s, nullptr, true,
@@ -503,8 +498,8 @@ FloatDecompressStatus sparseDecompressT(StackDeviceMemory& res,
                                         const BatchDesc& in, const BatchDesc& out,
                                         uint32_t maxCap, uint8_t* outSuccess_dev,
                                         uint32_t* outSize_dev, hipStream_t s) {
-  // chunk rows padded to 4 counts (16 B), for k_sparseChunkScan's vectors
-  const uint32_t chunks = roundUp(std::max(1u, divUp(maxCap, kChunkWords)), 4);
+  const uint32_t chunks = std::max(1u, divUp(maxCap, kChunkWords));
+  const uint32_t cblocks = divUp(chunks, kThreads);  // k_sparseChunks workgroups per element
   auto densePtrs = res.alloc<uint64_t>(s, nb);
   auto sizes = res.alloc<uint32_t>(s, nb);
   auto denseOk = res.alloc<uint8_t>(s, nb);
@@ -512,13 +507,12 @@ FloatDecompressStatus sparseDecompressT(StackDeviceMemory& res,
   auto list = res.alloc<uint8_t>(s, size_t(nb) * listStride);
   const BatchDesc lists = BatchDesc::strided(list.data(), listStride, maxCap + 1);
   auto chunkPre = res.alloc<uint32_t>(s, size_t(nb) * chunks);
+  auto blockTot = res.alloc<uint32_t>(s, size_t(nb) * cblocks);
   for (uint32_t y0 = 0; y0 < nb; y0 += kMaxGridY) {
     const uint32_t ny = std::min(kMaxGridY, nb - y0);
     prof::Scope p("sparse", s);
-    k_sparseChunks<<<dim3(divUp(chunks, kThreads), ny), kThreads, 0, s>>>(in, y0, chunks, densePtrs.data(),
-                                                                          sizes.data(), chunkPre.data());
-    HIP_LAUNCH_CHECK();
-    k_sparseChunkScan<<<ny, kThreads, 0, s>>>(y0, chunks, sizes.data(), chunkPre.data());
+    k_sparseChunks<<<dim3(cblocks, ny), kThreads, 0, s>>>(in, y0, chunks, cblocks, densePtrs.data(), sizes.data(),
+                                                          chunkPre.data(), blockTot.data());
     HIP_LAUNCH_CHECK();
   }
   // dense decode of the nonzero list (capacity: the largest output)
@@ -548,7 +542,8 @@ FloatDecompressStatus sparseDecompressT(StackDeviceMemory& res,
     const uint32_t ny = std::min(kMaxGridY, nb - y0);
     prof::Scope p("sparse", s);
     k_sparseExpand<FT><<<dim3(divUp(chunks, kWaves), ny), kThreads, 0, s>>>(
-        in, out, y0, chunks, sizes.data(), chunkPre.data(), lists, denseOk.data(), outSuccess_dev, outSize_dev);
+        in, out, y0, chunks, cblocks, sizes.data(), chunkPre.data(), blockTot.data(), lists, denseOk.data(),
+        outSuccess_dev, outSize_dev);
     HIP_LAUNCH_CHECK();
   }
   return status;

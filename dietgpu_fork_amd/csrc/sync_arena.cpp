@@ -125,8 +125,11 @@ SyncLease::SyncLease(StackDeviceMemory& res, hipStream_t stream, const size_t (&
   }
   for (int k = 0; k < kSyncRegions; ++k) base[k] = a->ptr[k];
   epoch = a->epoch;
-  if (rowsBytes) {  // buffer epoch & 1 now, the other one for the next call
-    const uint32_t mine = a->epoch & 1u;
+  if (rowsBytes) {
+    // the buffer already zeroed (by the previous such call) if there is one,
+    // else buffer epoch & 1; the other one is zeroed for the next call
+    uint32_t mine = a->epoch & 1u;
+    if (a->rowsClean[mine] < rowsBytes && a->rowsClean[mine ^ 1u] >= rowsBytes) mine ^= 1u;
     const size_t half = a->bytes[kSyncRows] / 2;
     rows[0] = static_cast<uint8_t*>(a->ptr[kSyncRows]) + mine * half;
     rows[1] = static_cast<uint8_t*>(a->ptr[kSyncRows]) + (mine ^ 1u) * half;

@@ -39,12 +39,15 @@ constexpr uint32_t kEpochMask = 0xffffu;
 // kSyncArrive holds the three-kernel path's last-arrival counters (NormArgs,
 // encode.h): untagged, they wrap back to zero at every element's last
 // arrival, so they are zero between calls.  kSyncRows holds two buffers of
-// histogram rows that k_hist accumulates with atomics for the encoder's
-// prologue normalisation (small three-kernel grids): a call uses buffer
-// epoch & 1, which must start zeroed, and its k_hist zeroes the other one
-// for the next call (SyncLease::rows).
+// histogram rows that k_hist (and the sparse compressor's k_sparseCount)
+// accumulate with atomics for the dense encoder's normalisation: a call uses
+// a buffer that must start zeroed -- the one the previous such call zeroed,
+// whatever the epochs of the calls in between -- and its kernel zeroes the
+// other one for the next call (SyncLease::rows).
 enum SyncRegion : int { kSyncCounters = 0, kSyncFlags, kSyncPartials, kSyncLog, kSyncArrive, kSyncRows,
                         kSyncRegions };
+// A lease that needs no region (only, say, histogram rows).
+constexpr size_t kNoSyncRegions[kSyncRegions] = {};
 // kSyncCounters layout: k_pcompress's two u64 dequeue counters.
 constexpr size_t kSyncCounterBytes = 16;
 

@@ -68,6 +68,18 @@ void testHistogram(StackDeviceMemory& res, hipStream_t s, uint32_t nb, const voi
   HIP_LAUNCH_CHECK();
 }
 
+// magic[q] for q = 0 .. 2048 by the compressors' in-register computation
+__global__ __launch_bounds__(256) void k_encMagic(uint32_t* magic) {
+  const uint32_t q = blockIdx.x * 256 + threadIdx.x;
+  if (q > (1u << 11)) return;
+  G(magic)[q] = q == 0 ? 0u : q == 1 ? 0xffffffffu : encMagicReg(q, 31 - __clz(q - 1));
+}
+
+void testEncMagic(hipStream_t s, uint32_t* magic) {
+  k_encMagic<<<divUp((1u << 11) + 1, 256), 256, 0, s>>>(magic);
+  HIP_LAUNCH_CHECK();
+}
+
 void testOccupy(hipStream_t s, uint32_t micros, uint32_t workgroups, uint32_t ldsBytes) {
   DG_CHECK(ldsBytes >= 1024 && ldsBytes <= 160 * 1024, "ldsBytes out of range");
   DG_CHECK(micros <= 1000000, "at most 1 s");
@@ -109,6 +121,10 @@ int dietgpu_test_histogram(dietgpu_stack* res, uint32_t nb, const void* in_dev, 
     DG_CHECK(res && res->mem, "null dietgpu_stack");
     dietgpu::testHistogram(*res->mem, reinterpret_cast<hipStream_t>(stream), nb, in_dev, size, stride, hist_dev);
   });
+}
+
+int dietgpu_test_enc_magic(uint32_t* magic_dev, void* stream) {
+  return guardedTest([&] { dietgpu::testEncMagic(reinterpret_cast<hipStream_t>(stream), magic_dev); });
 }
 
 }  // extern "C"

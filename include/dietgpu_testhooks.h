@@ -33,6 +33,14 @@ int dietgpu_test_occupy(void* stream, uint32_t micros, uint32_t workgroups, uint
 int dietgpu_test_histogram(dietgpu_stack* res, uint32_t nb, const void* in_dev, uint32_t size,
                            uint32_t stride, uint32_t* hist_dev, void* stream);
 
+/* magic_dev[q] (q = 0 .. 2048) = the 32-bit division magic of pdf q as the
+ * compressors compute it in registers (encMagicReg, csrc/encode.h: v_rcp_f64,
+ * two Newton steps, an exact fix-up); q 0 -> 0, q 1 -> 0xffffffff.  Checked
+ * against the closed form ceil(2^(32 + ceil(log2 q) - 1) / q) by the GPU tests;
+ * the magic replaces the division x / pdf of the reference's encode step
+ * (ans/GpuANSEncode.cuh:63-89). */
+int dietgpu_test_enc_magic(uint32_t* magic_dev, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -182,3 +182,48 @@ def test_three_kernel_rows_back_to_back(env):
                 assert sz[i] == ref.size, (k, i, sz[i], ref.size)
                 np.testing.assert_array_equal(host[i, : ref.size], ref, err_msg=f"call {k} element {i}")
     assert C.device_error_count(reset=True) == 0
+
+
+def test_sparse_rows_interleaved_with_three_kernel(env):
+    """The single-element sparse compressor counts its list's histogram into
+    the same arena row buffers (k_sparseCount, no zeroing launch) and zeroes
+    the other buffer for the next call; it takes one epoch, the dense codec
+    after it another, so the row buffers no longer follow epoch parity.
+    Interleave sparse calls of different sizes (1 to 64 rows per element,
+    fp32 and fp64: one and two segments) with three-kernel dense calls on
+    one stream; every archive (sentinel-filled) must equal the oracle's."""
+    N, C = env
+    from tests.util import sparsify
+
+    ws = C.Workspace(256 << 20)
+    s = torch.cuda.Stream()
+    tdt = {1: torch.int16, 2: torch.int16, 3: torch.int32, 4: torch.int64}
+    ndt = {1: np.int16, 2: np.int16, 3: np.int32, 4: np.int64}
+    fdt = {3: torch.float32, 4: torch.float64}
+    steps = [("sparse", 3, 1, 3_000_000, 0.9), ("dense", 2, 3, 12_000, 0), ("sparse", 3, 1, 5_000, 0.5),
+             ("sparse", 4, 1, 700_000, 0.8), ("dense", 4, 2, 300_000, 0), ("sparse", 3, 1, 300_000, 0.5),
+             ("sparse", 3, 1, 3_000_000, 0.9), ("dense", 3, 5, 40_000, 0), ("sparse", 4, 1, 9_000, 0.3)]
+    C.device_error_count(reset=True)
+    with C.compress_path("three-kernel"), torch.cuda.stream(s):
+        for k, (kind, ft, nb, n, frac) in enumerate(steps):
+            if kind == "sparse":
+                w = sparsify(float_words(ft, n, seed=500 + k), frac_zero=frac, seed=600 + k)
+                ref = O.sparse_compress(w, ft)
+                x = torch.from_numpy(w.view(ndt[ft])).to(DEV).view(fdt[ft])
+                out, sizes = C.sparse_compress([x], ws=ws)
+                s.synchronize()
+                assert int(sizes[0]) == ref.size, (k, int(sizes[0]), ref.size)
+                np.testing.assert_array_equal(out[0, : ref.size].cpu().numpy(), ref, err_msg=f"step {k}")
+            else:
+                words = [float_words(ft, n, seed=700 * k + i) for i in range(nb)]
+                x = torch.from_numpy(np.stack(words).view(ndt[ft])).to(DEV)
+                out = torch.full([nb, C.max_float_compressed_size(ft, n)], SENTINEL, dtype=torch.uint8, device=DEV)
+                sizes = torch.empty([nb], dtype=torch.int32, device=DEV)
+                C.float_compress_stride(x.view(tdt[ft]), ft=ft, ws=ws, out=out, sizes=sizes)
+                s.synchronize()
+                host, sz = out.cpu().numpy(), sizes.cpu().tolist()
+                for i, ww in enumerate(words):
+                    ref = O.float_compress(ww, ft)
+                    assert sz[i] == ref.size, (k, i, sz[i], ref.size)
+                    np.testing.assert_array_equal(host[i, : ref.size], ref, err_msg=f"step {k} element {i}")
+    assert C.device_error_count(reset=True) == 0

@@ -90,6 +90,16 @@ def test_normalization_kat(C, ws, G, name, path, offset):
 HIST_SIZES = [1, 2, 11, 32, 55, 1000, 1001, 1000000, 1024 * 1024, 1000001, 12345677]
 
 
+def test_enc_magic_exhaustive(C):
+    """The encode step's division x / pdf (ans/GpuANSEncode.cuh:63-89) is a
+    multiply-high by a 32-bit magic computed in registers by every
+    normalisation (v_rcp_f64, two Newton steps, exact fix-up): equal to the
+    closed form ceil(2^(32 + ceil(log2 q) - 1) / q) for every pdf q <= 2^11."""
+    got = C.test_enc_magic().numpy()
+    want = [0, 0xFFFFFFFF] + [-(-(1 << (32 + (q - 1).bit_length() - 1)) // q) for q in range(2, (1 << 11) + 1)]
+    assert got.tolist() == want
+
+
 @pytest.mark.parametrize("size", HIST_SIZES)
 def test_histogram_batch(C, ws, size):
     nb, pad = 3, 11  # ANSStatisticsTest.cu:61-78
