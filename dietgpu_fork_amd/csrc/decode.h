@@ -365,7 +365,7 @@ __device__ __forceinline__ void buildLut64(gp<const uint16_t> pdfIn, lp<u32x2> l
 // second generation.  (fp64, VGPR-bound at four workgroups per CU, spills a
 // few SGPRs to VGPR lanes instead: its decode time is unchanged.)
 template <int FT, int KK, bool NT, bool BAL>
-__global__ __launch_bounds__(dec::kThreads) __attribute__((amdgpu_num_sgpr(80), amdgpu_waves_per_eu(FT == 1 || FT == 2 ? 8 : 4))) void k_decode(const InlineTable,
+__global__ __launch_bounds__(dec::kThreads) __attribute__((amdgpu_num_sgpr(80), amdgpu_waves_per_eu(4))) void k_decode(const InlineTable,
                                                           BatchDesc in, BatchDesc out,
                                                           uint32_t batchOffset, int pb,
                                                           uint32_t chunksPerWG,
@@ -435,7 +435,7 @@ __global__ __launch_bounds__(dec::kThreads) __attribute__((amdgpu_num_sgpr(80), 
   uint32_t x0[K][S];
   uint2 bwE[K][S][2];
   uint32_t rvA[K][R], rvB[K][R];
-  auto issueRaw = [&](uint32_t blk0) __attribute__((always_inline)) {
+  auto issue = [&](uint32_t blk0) __attribute__((always_inline)) {
     const uint32_t off = dec::kChunk * l;
 #pragma unroll
     for (int c = 0; c < K; ++c) {
@@ -446,13 +446,6 @@ __global__ __launch_bounds__(dec::kThreads) __attribute__((amdgpu_num_sgpr(80), 
                                  blk0 + 2 * c < nBlocks ? min(kBlockSize, n - (blk0 + 2 * c) * kBlockSize) : 0u);
       if (FT != 0 && vecIO && uwMin == kBlockSize)
         Join<FT>::load(rvA[c], raw, n, bkMine * kBlockSize + (kBlockSize / 32 / dec::kSegSteps - 1) * dec::kSegWords + off);
-    }
-  };
-  auto issue = [&](uint32_t blk0) __attribute__((always_inline)) {
-    issueRaw(blk0);
-#pragma unroll
-    for (int c = 0; c < K; ++c) {
-      const uint32_t bkMine = blk0 + 2 * c + (lane >> 5);
 #pragma unroll
       for (int s = 0; s < S; ++s) {
         gp<const uint8_t> states = arch[s] + kANSHeaderBytes + kPdfBytes;
@@ -478,32 +471,12 @@ __global__ __launch_bounds__(dec::kThreads) __attribute__((amdgpu_num_sgpr(80), 
     __syncthreads();
   }
 
-  // The next pass's initial states and blockWords (one pair, one stream)
-  // are loaded at the start of the current pass, so that the next pass's
-  // ring fill goes out at once: one dependent round trip fewer per pass
-  // after the first (cold archives).  Two VGPRs: the four blockWords dwords
-  // ride in lanes 0-3 of one register.
-  constexpr bool kPre = K == 1 && S == 1;
-  uint32_t x0N = kMinState, bwN = 0;
-  bool haveN = false;
-
   // Persistent over chunksPerWG consecutive chunks of this element (the grid
   // is one generation of resident workgroups; one table build per WG).
   for (uint32_t pass = 0; pass < chunksPerWG; ++pass) {
     const uint32_t blk0 = (blockIdx.x * chunksPerWG + pass) * Cfg::kBlocksPerWG + w * Cfg::kBlocksPerWave;
     if (blk0 >= nBlocks) break;
-    if (pass > 0) {
-      if (kPre && haveN) {
-        issueRaw(blk0);
-        x0[0][0] = x0N;
-#pragma unroll
-        for (int hh = 0; hh < 2; ++hh)
-          bwE[0][0][hh] = make_uint2(uint32_t(__builtin_amdgcn_readlane(int(bwN), 2 * hh)),
-                                     uint32_t(__builtin_amdgcn_readlane(int(bwN), 2 * hh + 1)));
-      } else {
-        issue(blk0);
-      }
-    }
+    if (pass > 0) issue(blk0);
 
     // per pair c: blocks blk0 + 2c (lanes 0-31) and blk0 + 2c + 1 (lanes 32-63)
     uint32_t uwH[K][2];  // wave-uniform: block sizes follow from n alone
@@ -569,21 +542,6 @@ __global__ __launch_bounds__(dec::kThreads) __attribute__((amdgpu_num_sgpr(80), 
           }
         }
         d.x = x0[c][s];
-      }
-    }
-
-    // the next pass's states and blockWords (see kPre)
-    haveN = false;
-    if constexpr (kPre) {
-      const uint32_t blkN = blk0 + Cfg::kBlocksPerWG;
-      if (pass + 1 < chunksPerWG && blkN < nBlocks) {
-        gp<const uint8_t> states = arch[0] + kANSHeaderBytes + kPdfBytes;
-        gp<const uint32_t> bwd = (gp<const uint32_t>)(states + uint64_t(kStateBytesPerBlock) * nBlocks);
-        const uint32_t bkMine = blkN + (lane >> 5);
-        x0N = bkMine < nBlocks ? ((gp<const uint32_t>)(states + uint64_t(kStateBytesPerBlock) * bkMine))[l]
-                               : kMinState;
-        bwN = lane < 4 && blkN + (lane >> 1) < nBlocks ? bwd[2 * (blkN + (lane >> 1)) + (lane & 1)] : 0u;
-        haveN = true;
       }
     }
 

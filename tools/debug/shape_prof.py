@@ -5,7 +5,8 @@ roundtrip bit for bit, then runs `reps` compress + decompress calls
 back to back and prints whole-call times (events on the launch stream).
     usage: python tools/debug/shape_prof.py SHAPE [reps]
 SHAPE: c3 | raw_bf16_b | raw_bf16_nb | raw_fp32_b | fp64_16m | fp64_1e8 |
-       sp_fp64_5x15m | sp_fp32_5x15m | sp_fp32_1x15m90 | c2 | c5 | bf16_1e9"""
+       sp_fp64_5x15m | sp_fp32_5x15m | sp_fp32_1x15m90 | c2 | c5 | bf16_1e9 |
+       bf16_16m | bf16_1m | fp32_16m"""
 import os
 import sys
 
@@ -91,6 +92,20 @@ def build(shape, ws):
         return (lambda: C.float_compress_stride(x, ws=ws, out=arch, sizes=sizes),
                 lambda: C.float_decompress_stride(arch, n, torch.bfloat16, ws=ws, out=y),
                 lambda: torch.equal(x.view(torch.int16), y.view(torch.int16)))
+    if shape in ("bf16_16m", "bf16_1m", "fp32_16m"):
+        # batch-1 pointer-API calls (the bench's batch-1 sweep, FloatBenchmark.cu)
+        n = 16_000_000 if shape.endswith("16m") else 1_000_000
+        g = torch.Generator(device=DEV).manual_seed(6)
+        x = torch.randn(n, generator=g, device=DEV)
+        if shape.startswith("bf16"):
+            x = (x.view(torch.int32) >> 16).to(torch.int16).view(torch.bfloat16)
+        arch, _ = C.float_compress_pointer([x], prob_bits=10, ws=ws)
+        y = torch.empty_like(x)
+        row = [arch[0]]
+        iv = torch.int16 if shape.startswith("bf16") else torch.int32
+        return (lambda: C.float_compress_pointer([x], prob_bits=10, ws=ws),
+                lambda: C.float_decompress_pointer(row, [y], prob_bits=10, ws=ws),
+                lambda: torch.equal(x.view(iv), y.view(iv)))
     if shape == "c2":
         g = torch.Generator(device=DEV).manual_seed(0)
         x32 = torch.randn(256, 524288, generator=g, device=DEV)
