@@ -133,6 +133,72 @@ def test_float_split_size_parity(C, N, ws, ft, checksum):
     assert torch.equal(dec, t)
 
 
+@pytest.mark.parametrize("checksum", [False, True])
+@pytest.mark.parametrize("n", [70001, 1_000_000])
+def test_single_element_table_apis(C, N, ws, n, checksum):
+    """One-element pointer and split-size calls: the three-kernel path gets
+    stride descriptors of that element instead of an uploaded table
+    (DeviceDescs, codec.hip), for the encoder, the float checksum view and
+    the decoder's checksum verification alike.  The element sits at a 2-byte
+    offset (not 16 B-aligned: always the three-kernel path) and, for the
+    float codecs, in every float type; archives equal the oracle's, roundtrips
+    are exact (ans/GpuANSCodec.h:93-167, float/GpuFloatCodec.h:92-160)."""
+    L = N.lib()
+    data = exp_bytes(n + 2, lam=10.0, seed=n % 97)
+    buf = torch.from_numpy(data).to(DEV)
+    ref = O.ans_encode(data[2:], 10, checksum)
+    # pointer API
+    arch, osz = C.ans_encode_pointer([buf[2:]], checksum=checksum, ws=ws)
+    assert int(osz[0]) == ref.size
+    np.testing.assert_array_equal(arch[0][: ref.size].cpu().numpy(), ref)
+    y = torch.empty(n, dtype=torch.uint8, device=DEV)
+    ok, dsz = C.ans_decode_pointer([arch[0][: ref.size].clone()], [y], checksum=checksum, ws=ws)
+    assert ok.cpu().tolist() == [1] and dsz.cpu().tolist() == [n] and torch.equal(y, buf[2:])
+    # split-size API (one split: the whole buffer from a 4 B-aligned base)
+    cols = C.max_compressed_size(n + 2)
+    out = torch.empty([1, cols], dtype=torch.uint8, device=DEV)
+    N.check(L.dietgpu_ans_encode_batch_split_size(ws.h, 10, int(checksum), 1, buf.data_ptr(),
+                                                  N.u32_array([n + 2]), None, out.data_ptr(), cols,
+                                                  osz.data_ptr(), _s()))
+    ref2 = O.ans_encode(data, 10, checksum)
+    assert int(osz[0]) == ref2.size
+    np.testing.assert_array_equal(out[0, : ref2.size].cpu().numpy(), ref2)
+    dec = torch.empty(n + 2, dtype=torch.uint8, device=DEV)
+    row = out[0, : ref2.size].clone()
+    N.check(L.dietgpu_ans_decode_batch_split_size(ws.h, 10, int(checksum), 1, N.ptr_array([row.data_ptr()]),
+                                                  dec.data_ptr(), N.u32_array([n + 2]), ok.data_ptr(),
+                                                  dsz.data_ptr(), _s()))
+    assert ok.cpu().tolist() == [1] and torch.equal(dec, buf)
+    for ft in (1, 2, 3, 4):
+        wb = WORD_BYTES[ft]
+        words = float_words(ft, n + 1, seed=ft + n % 13)
+        t = torch.from_numpy(words.view(NP_SIGNED[ft]).copy()).to(DEV)
+        x = t[1:].view(TORCH_FLOAT[ft])  # one word in: not 16 B-aligned
+        fref = O.float_compress(words[1:], ft, 10, checksum)
+        farch, fsz = C.float_compress_pointer([x], ft=ft, checksum=checksum, ws=ws)
+        assert int(fsz[0]) == fref.size, ft
+        np.testing.assert_array_equal(farch[0][: fref.size].cpu().numpy(), fref, err_msg=f"ft {ft}")
+        fy = torch.empty_like(x)
+        ok, dsz = C.float_decompress_pointer([farch[0][: fref.size].clone()], [fy], ft=ft, checksum=checksum,
+                                             ws=ws)
+        assert ok.cpu().tolist() == [1] and dsz.cpu().tolist() == [n], ft
+        assert torch.equal(fy.view(TORCH_WORD[ft]), t[1:]), ft
+        # split-size API: one split from an unaligned base
+        fcols = C.max_float_compressed_size(ft, n)
+        fout = torch.empty([1, fcols], dtype=torch.uint8, device=DEV)
+        N.check(L.dietgpu_float_compress_split_size(ws.h, ft, 10, int(checksum), 1, t.data_ptr() + wb,
+                                                    N.u32_array([n]), fout.data_ptr(), fcols, fsz.data_ptr(),
+                                                    _s()))
+        assert int(fsz[0]) == fref.size, ft
+        np.testing.assert_array_equal(fout[0, : fref.size].cpu().numpy(), fref, err_msg=f"split ft {ft}")
+        fdec = torch.empty(n + 1, dtype=TORCH_WORD[ft], device=DEV)
+        frow = fout[0, : fref.size].clone()
+        N.check(L.dietgpu_float_decompress_split_size(ws.h, ft, 10, int(checksum), 1, N.ptr_array([frow.data_ptr()]),
+                                                      fdec.data_ptr() + wb, N.u32_array([n]), ok.data_ptr(),
+                                                      dsz.data_ptr(), _s()))
+        assert ok.cpu().tolist() == [1] and torch.equal(fdec[1:], t[1:]), ft
+
+
 def test_reference_ans_split_tests(C):
     """ans_test.py:79-139 (test_split_compress / test_split_decompress): byte
     mode, checksum on, 64 MiB temp memory, through torch.ops.dietgpu."""
