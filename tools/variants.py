@@ -548,6 +548,16 @@ VARS["nostep"] = [(EH, "for (int s = 0; s < S; ++s) encStep<false, R>(st[c][s], 
                    "for (int s = 0; s < S; ++s) st[c][s].x += E[u][c][s].z;"),
                   (P, "for (uint32_t u = 0; u < enc::kUnroll; ++u) encStep<false, pc::kRing>(p, true, Ev[u], hv);",
                    "for (uint32_t u = 0; u < enc::kUnroll; ++u) p.x += Ev[u].z;")]
+# round 6: the decoder's archive reads streamed (read once per call): raw
+# float bytes / compressed words as nontemporal loads
+DEC = "decode.h"
+DNT_RAW = [(DEC, "      const uint2 a = ld8(raw + i0);",
+            "      const u32x2 a_ = __builtin_nontemporal_load((gp<const u32x2>)(raw + i0)); const uint2 a = make_uint2(a_.x, a_.y);"),
+           (DEC, "      const uint4 a = ld16(raw + 2 * i0);", "      const uint4 a = ld16nt(raw + 2 * i0);")]
+DNT_RING = [(DEC, "  if (vec) return *(gp<const u32x2>)p;", "  if (vec) return __builtin_nontemporal_load((gp<const u32x2>)p);")]
+VARS["dnt_raw"] = DNT_RAW
+VARS["dnt_ring"] = DNT_RING
+VARS["dnt_both"] = DNT_RAW + DNT_RING
 if sys.argv[1:] == ["--check"]:
     for name, subs in VARS.items():
         live = all(os.path.exists(f"{REPO}/dietgpu_fork_amd/csrc/{f}") and
