@@ -555,7 +555,7 @@ template <int FT>
 void decodeBatchDevice(StackDeviceMemory& res, int pb, uint32_t nb, const BatchDesc& in,
                        const BatchDesc& out, uint32_t maxCapacity, uint8_t* outSuccess_dev,
                        uint32_t* outSize_dev, hipStream_t s, const DeviceTables* tabs = nullptr,
-                       bool streamOut = true) {
+                       bool streamOut = true, bool capacityOnly = false) {
   checkProbBits(pb);
   if (nb == 0) return;
   const uint32_t maxBlocks = divUp(maxCapacity, kBlockSize);
@@ -576,8 +576,14 @@ void decodeBatchDevice(StackDeviceMemory& res, int pb, uint32_t nb, const BatchD
       const uint32_t chunks = std::max(1u, divUp(maxBlocks, Cfg::kBlocksPerWG));
       const uint32_t slots =
           residentSlots(reinterpret_cast<const void*>(&k_decode<FT, KK, NT, true>), dec::kThreads, lds);
-      const uint32_t P = std::min(kMaxDecodeChunks,
-                                  std::max(1u, uint32_t((uint64_t(chunks) * ny + slots / 2) / slots)));
+      // capacityOnly: the capacity is all the host knows and may far exceed
+      // the archives' sizes (the sparse codec's nonzero lists): one chunk per
+      // workgroup, so the chunks that exist run side by side instead of P
+      // passes of a workgroup while the grid's upper part exits at once
+      // (5 x 15M fp32 at 50 % zeros: the list decode 77 -> see DESIGN)
+      const uint32_t P = capacityOnly ? 1u
+                                      : std::min(kMaxDecodeChunks,
+                                                 std::max(1u, uint32_t((uint64_t(chunks) * ny + slots / 2) / slots)));
       dim3 g(divUp(chunks, P), ny);
       // remaining-work wave priorities balance the finish of a single
       // generation (c2 decode −2 %); across several generations they cost
@@ -880,23 +886,24 @@ FloatDecompressStatus floatDecompressDescs(StackDeviceMemory& res,
                                            const FloatDecompressConfig& config, uint32_t nb,
                                            const BatchDesc& in, const BatchDesc& out,
                                            uint32_t maxCap, uint8_t* succ, uint32_t* sizes,
-                                           hipStream_t s, const DeviceTables* tabs, bool streamOut) {
+                                           hipStream_t s, const DeviceTables* tabs, bool streamOut,
+                                           bool capacityOnly) {
   checkFloatConfig(config);
   const int pb = config.ansConfig.probBits;
   // streaming output stores unless the output is read back (checksum)
   const bool nt = streamOut && !config.useChecksum;
   switch (config.floatType) {
     case FloatType::kFloat16:
-      decodeBatchDevice<1>(res, pb, nb, in, out, maxCap, succ, sizes, s, tabs, nt);
+      decodeBatchDevice<1>(res, pb, nb, in, out, maxCap, succ, sizes, s, tabs, nt, capacityOnly);
       break;
     case FloatType::kBFloat16:
-      decodeBatchDevice<2>(res, pb, nb, in, out, maxCap, succ, sizes, s, tabs, nt);
+      decodeBatchDevice<2>(res, pb, nb, in, out, maxCap, succ, sizes, s, tabs, nt, capacityOnly);
       break;
     case FloatType::kFloat32:
-      decodeBatchDevice<3>(res, pb, nb, in, out, maxCap, succ, sizes, s, tabs, nt);
+      decodeBatchDevice<3>(res, pb, nb, in, out, maxCap, succ, sizes, s, tabs, nt, capacityOnly);
       break;
     default:
-      decodeBatchDevice<4>(res, pb, nb, in, out, maxCap, succ, sizes, s, tabs, nt);
+      decodeBatchDevice<4>(res, pb, nb, in, out, maxCap, succ, sizes, s, tabs, nt, capacityOnly);
       break;
   }
   FloatDecompressStatus status;

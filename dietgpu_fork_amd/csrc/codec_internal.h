@@ -43,7 +43,7 @@ FloatDecompressStatus floatDecompressDescs(StackDeviceMemory& res,
                                            const BatchDesc& in, const BatchDesc& out,
                                            uint32_t maxCap, uint8_t* succ, uint32_t* sizes,
                                            hipStream_t s, const DeviceTables* tabs = nullptr,
-                                           bool streamOut = true);
+                                           bool streamOut = true, bool capacityOnly = false);
 
 // Compare archive checksums with the XOR of `decoded.size(b)` bytes of each
 // decoded element; synchronises `s`.

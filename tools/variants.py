@@ -558,6 +558,9 @@ DNT_RING = [(DEC, "  if (vec) return *(gp<const u32x2>)p;", "  if (vec) return _
 VARS["dnt_raw"] = DNT_RAW
 VARS["dnt_ring"] = DNT_RING
 VARS["dnt_both"] = DNT_RAW + DNT_RING
+# the sparse compressor counting the list histogram for every batch (not only
+# one element), the dense codec then skipping its k_hist pass over the lists
+VARS["sphistall"] = [(SPX, "  bool countHist = nb == 1;", "  bool countHist = nb <= 64;")]
 if sys.argv[1:] == ["--check"]:
     for name, subs in VARS.items():
         live = all(os.path.exists(f"{REPO}/dietgpu_fork_amd/csrc/{f}") and
