@@ -561,6 +561,28 @@ VARS["dnt_both"] = DNT_RAW + DNT_RING
 # the sparse compressor counting the list histogram for every batch (not only
 # one element), the dense codec then skipping its k_hist pass over the lists
 VARS["sphistall"] = [(SPX, "  bool countHist = nb == 1;", "  bool countHist = nb <= 64;")]
+# round 6: 4-byte decode-table entries {sym:8 | pdf:12 | slot - cdf:12}
+# (half the LDS bytes of the step's table gather, two more VALU per step)
+VARS["lut32"] = [
+    (DEC, "  __host__ __device__ static constexpr uint32_t lutBytes(int pb) { return S * (8u << pb); }",
+     "  __host__ __device__ static constexpr uint32_t lutBytes(int pb) { return S * (4u << pb); }"),
+    (DEC, """  const u32x2 e = lut[p.x & mask];
+  uint32_t xn = __umul24(e.x, p.x >> pb) + e.y;""",
+     """  const uint32_t e = ((lp<const uint32_t>)lut)[p.x & mask];
+  uint32_t xn = __umul24(__builtin_amdgcn_ubfe(e, 12, 12), p.x >> pb) + (e & 0xfffu);"""),
+    (DEC, "  return e.x;\n}", "  return e;\n}"),
+    (DEC, """  u32x2 e[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) e[c] = lut[c][p[c]->x & mask];""",
+     """  uint32_t e[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) e[c] = ((lp<const uint32_t>)lut[c])[p[c]->x & mask];"""),
+    (DEC, "    xn[c] = __umul24(e[c].x, q.x >> pb) + e[c].y;",
+     "    xn[c] = __umul24(__builtin_amdgcn_ubfe(e[c], 12, 12), q.x >> pb) + (e[c] & 0xfffu);"),
+    (DEC, "    e0[c] = e[c].x;", "    e0[c] = e[c];"),
+    (DEC, "      if (slot < total) lut[slot] = u32x2{pdfS[s[j]] | (s[j] << 24), slot - cs[j]};",
+     "      if (slot < total) ((lp<uint32_t>)lut)[slot] = (s[j] << 24) | (pdfS[s[j]] << 12) | (slot - cs[j]);"),
+]
 if sys.argv[1:] == ["--check"]:
     for name, subs in VARS.items():
         live = all(os.path.exists(f"{REPO}/dietgpu_fork_amd/csrc/{f}") and
