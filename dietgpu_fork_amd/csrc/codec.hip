@@ -32,10 +32,20 @@ namespace dietgpu {
 namespace {
 constexpr uint32_t kMaxGridY = 65535;
 
-uint32_t histChunkWords(uint32_t nb, uint32_t maxSize) {
+// k_hist chunk (words): 4 K .. 64 K words, halved while the batch has fewer
+// than 2,048 chunks -- for single-segment formats only down to 16 K words
+// once there are 512: a k_hist workgroup zeroes and sums 32 KB of LDS
+// counters, which 4 K- or 8 K-word chunks do not amortise (1 x 16M bf16
+// compress 41.6 -> 37.0 us, fp32 48.2 -> 46.3 us, same box; 1e8-word
+// elements keep their 32 K-word chunks, 64 K measured slower).  fp64's two
+// 16-column counter sets keep the 2,048 rule.
+uint32_t histChunkWords(uint32_t nb, uint32_t maxSize, int segs) {
   uint32_t chunk = 64 * 1024;
-  const uint32_t target = 2048;
-  while (chunk > 4096 && uint64_t(nb) * divUp(std::max(maxSize, 1u), chunk) < target) chunk /= 2;
+  auto enough = [&](uint32_t c) {
+    const uint64_t total = uint64_t(nb) * divUp(std::max(maxSize, 1u), c);
+    return total >= 2048 || (segs == 1 && c <= 16 * 1024 && total >= 512);
+  };
+  while (chunk > 4096 && !enough(chunk)) chunk /= 2;
   while (divUp(maxSize, chunk) > 4096) chunk *= 2;
   return chunk;
 }
@@ -372,7 +382,7 @@ void encodeBatchDevice(StackDeviceMemory& res, int pb, bool useChecksum, uint32_
   const bool userHist = FT == 0 && hist_dev != nullptr;
   const bool preHist = FT != 0 && pre != nullptr;  // partial rows counted by the caller
   const bool preNorm = preHist && pre->table != nullptr;  // ... and normalised
-  const uint32_t chunkWords = histChunkWords(nb, maxSize);
+  const uint32_t chunkWords = histChunkWords(nb, maxSize, kSegs);
   const uint32_t chunks = preHist ? std::max(1u, pre->nRows) : std::max(1u, divUp(maxSize, chunkWords));
   const bool runHist = !preHist && (!userHist || useChecksum);
   const bool rawCk = FT == 0 && useChecksum;

@@ -583,6 +583,9 @@ VARS["lut32"] = [
     (DEC, "      if (slot < total) lut[slot] = u32x2{pdfS[s[j]] | (s[j] << 24), slot - cs[j]};",
      "      if (slot < total) ((lp<uint32_t>)lut)[slot] = (s[j] << 24) | (pdfS[s[j]] << 12) | (slot - cs[j]);"),
 ]
+# round 6: fewer, larger k_hist chunks for mid-size batch-1 elements
+VARS["ht512"] = [("codec.hip", "  const uint32_t target = 2048;", "  const uint32_t target = 512;")]
+VARS["ht1024"] = [("codec.hip", "  const uint32_t target = 2048;", "  const uint32_t target = 1024;")]
 if sys.argv[1:] == ["--check"]:
     for name, subs in VARS.items():
         live = all(os.path.exists(f"{REPO}/dietgpu_fork_amd/csrc/{f}") and
